@@ -1,0 +1,467 @@
+// Python bindings of the CDNA4 kernels (module `neuronx_distributed_llama3_2_amd._C`).
+// Every entry point validates shapes/dtypes on the host BEFORE launching (a wrong shape must
+// never reach a hand-written kernel), then launches on the caller's current HIP stream, so the
+// ops compose with torch streams and hipGraph capture.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+namespace nxd {
+int flash_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, const int64_t*,
+                          const int64_t*, const int64_t*, int, int, int, int, int, int, float, int, int, hipStream_t);
+int flash_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*, float*, float*,
+                          void*, void*, void*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
+                          const int64_t*, const int64_t*, const int64_t*, const int64_t*, int, int, int, int, int, int,
+                          float, int, int, hipStream_t);
+int rmsnorm_fwd_launch(const void*, const void*, const void*, void*, void*, float*, int64_t, int, float, hipStream_t);
+int rmsnorm_bwd_num_partials(int64_t);
+int rmsnorm_bwd_launch(const void*, const void*, const void*, const float*, const void*, void*, float*, float*, int,
+                       int64_t, int, hipStream_t);
+int rope_inplace_launch(void*, int64_t, int64_t, int, int, int, const float*, const float*, const int64_t*, int64_t,
+                        int64_t, float, hipStream_t);
+int swiglu_fwd_launch(const void*, void*, int64_t, int, hipStream_t);
+int swiglu_bwd_launch(const void*, const void*, void*, int64_t, int, hipStream_t);
+int xent_stats_launch(const void*, int, const int64_t*, float*, int64_t, int, int64_t, int64_t, hipStream_t);
+int xent_bwd_launch(const void*, int, const int64_t*, const float*, void*, int64_t, int, int64_t, int64_t, int64_t, float,
+                    int64_t, hipStream_t);
+int flat_reduce_launch(const void*, int, int64_t, int, float*, float*, int, hipStream_t);
+int adamw_flat_launch(float*, const void*, int, float*, float*, void*, int64_t, float, float, float, float, float, float,
+                      float, const float*, float, hipStream_t);
+int clip_coef_launch(const float*, float*, float, int, hipStream_t);
+int scale_flat_launch(float*, int64_t, const float*, hipStream_t);
+int embedding_fwd_launch(const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, hipStream_t);
+int embedding_bwd_launch(const int64_t*, const void*, float*, int64_t, int, int64_t, int64_t, hipStream_t);
+int decode_attn_launch(const void*, const int64_t*, const void*, const void*, const int64_t*, const int*, const int*,
+                       float*, float*, float*, void*, const int64_t*, int, int, int, int, int, int, float, hipStream_t);
+int kv_cache_write_launch(const void*, const void*, const int64_t*, void*, void*, const int64_t*, const int*, const int*,
+                          int, int, int, int, int, hipStream_t);
+int argmax_launch(const void*, int, int64_t, int, int, int64_t*, hipStream_t);
+int topk_sample_launch(const void*, int, int64_t, int, int, int, float, const float*, int64_t*, float*, int64_t*,
+                       hipStream_t);
+}  // namespace nxd
+
+namespace {
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, what, " failed with code ", rc); }
+
+void check_cuda(const at::Tensor& t, const char* n) { TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor"); }
+
+void check_bf16(const at::Tensor& t, const char* n) {
+  check_cuda(t, n);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, n, " must be bfloat16");
+}
+
+void check_aligned16(const at::Tensor& t, const char* n) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, n, " must be 16-byte aligned");
+}
+
+// [B, S, H, D] view with unit stride on D and 16-B aligned rows
+void bshd_strides(const at::Tensor& t, const char* n, int64_t* s) {
+  check_bf16(t, n);
+  TORCH_CHECK(t.dim() == 4, n, " must be [B, S, H, D]");
+  TORCH_CHECK(t.stride(3) == 1, n, " must have unit stride on D");
+  for (int i = 0; i < 3; ++i) TORCH_CHECK(t.stride(i) % 8 == 0 || t.size(i) == 1, n, " strides must be multiples of 8 elements");
+  check_aligned16(t, n);
+  s[0] = t.stride(0);
+  s[1] = t.stride(1);
+  s[2] = t.stride(2);
+}
+
+void flash_attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse, double scale, bool causal,
+                    int64_t causal_offset) {
+  int64_t qs[3], ks[3], vs[3], os[3];
+  bshd_strides(q, "q", qs);
+  bshd_strides(k, "k", ks);
+  bshd_strides(v, "v", vs);
+  bshd_strides(o, "o", os);
+  const int B = q.size(0), Sq = q.size(1), Hq = q.size(2), D = q.size(3);
+  const int Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == Sk && v.size(2) == Hkv, "k/v shape mismatch");
+  TORCH_CHECK(k.size(3) == D && v.size(3) == D && o.sizes() == q.sizes(), "head dim / output shape mismatch");
+  TORCH_CHECK(D == 64 || D == 128, "head_dim must be 64 or 128");
+  TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0, "num q heads must be a multiple of num kv heads");
+  TORCH_CHECK(Sk > 0, "empty key sequence");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == (int64_t)B * Hq * Sq,
+              "lse must be contiguous fp32 [B, Hq, Sq]");
+  check_rc(nxd::flash_attn_fwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), qs, ks,
+                                      vs, os, B, Sq, Sk, Hq, Hkv, D, (float)scale, causal ? 1 : 0, (int)causal_offset,
+                                      cur_stream()),
+           "flash_attn_fwd");
+}
+
+void flash_attn_bwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor dout, at::Tensor lse,
+                    at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t causal_offset) {
+  int64_t qs[3], ks[3], vs[3], os[3], dos[3], dqs[3], dks[3], dvs[3];
+  bshd_strides(q, "q", qs);
+  bshd_strides(k, "k", ks);
+  bshd_strides(v, "v", vs);
+  bshd_strides(o, "o", os);
+  bshd_strides(dout, "dout", dos);
+  bshd_strides(dq, "dq", dqs);
+  bshd_strides(dk, "dk", dks);
+  bshd_strides(dv, "dv", dvs);
+  const int B = q.size(0), Sq = q.size(1), Hq = q.size(2), D = q.size(3);
+  const int Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(k.sizes() == v.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "k/v/dk/dv shape mismatch");
+  TORCH_CHECK(o.sizes() == q.sizes() && dout.sizes() == q.sizes() && dq.sizes() == q.sizes(), "q/o/dout/dq shape mismatch");
+  TORCH_CHECK(k.size(0) == B && k.size(3) == D, "k shape mismatch");
+  TORCH_CHECK(D == 64 || D == 128, "head_dim must be 64 or 128");
+  TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0, "num q heads must be a multiple of num kv heads");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == (int64_t)B * Hq * Sq, "bad lse");
+  auto opts = q.options().dtype(at::kFloat);
+  at::Tensor delta = at::empty({(int64_t)B * Hq * Sq}, opts);
+  at::Tensor dq_acc = at::empty({(int64_t)B * Hq * Sq * D}, opts);
+  check_rc(nxd::flash_attn_bwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
+                                      lse.data_ptr<float>(), delta.data_ptr<float>(), dq_acc.data_ptr<float>(), dq.data_ptr(),
+                                      dk.data_ptr(), dv.data_ptr(), qs, ks, vs, os, dos, dqs, dks, dvs, B, Sq, Sk, Hq, Hkv, D,
+                                      (float)scale, causal ? 1 : 0, (int)causal_offset, cur_stream()),
+           "flash_attn_bwd");
+}
+
+void rows_check(const at::Tensor& t, const char* n, int64_t H) {
+  check_bf16(t, n);
+  TORCH_CHECK(t.is_contiguous(), n, " must be contiguous");
+  TORCH_CHECK(t.size(-1) == H, n, " last dim mismatch");
+  check_aligned16(t, n);
+}
+
+void rmsnorm_fwd(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> h_out,
+                 at::Tensor rstd, double eps) {
+  const int64_t H = x.size(-1);
+  const int64_t rows = x.numel() / H;
+  rows_check(x, "x", H);
+  rows_check(y, "y", H);
+  check_bf16(w, "w");
+  TORCH_CHECK(w.is_contiguous() && w.numel() == H, "w must be [H]");
+  TORCH_CHECK(H % 8 == 0 && H <= 16384, "hidden size must be a multiple of 8 and <= 16384");
+  TORCH_CHECK(rstd.scalar_type() == at::kFloat && rstd.numel() == rows, "rstd must be fp32 [rows]");
+  const void* rp = nullptr;
+  void* hp = nullptr;
+  if (res.has_value()) {
+    rows_check(*res, "residual", H);
+    TORCH_CHECK(res->numel() == x.numel(), "residual shape mismatch");
+    TORCH_CHECK(h_out.has_value(), "h_out required with residual");
+    rows_check(*h_out, "h_out", H);
+    rp = res->data_ptr();
+    hp = h_out->data_ptr();
+  }
+  check_rc(nxd::rmsnorm_fwd_launch(x.data_ptr(), rp, w.data_ptr(), y.data_ptr(), hp, rstd.data_ptr<float>(), rows, (int)H,
+                                   (float)eps, cur_stream()),
+           "rmsnorm_fwd");
+}
+
+void rmsnorm_bwd(at::Tensor dy, at::Tensor h, at::Tensor w, at::Tensor rstd, c10::optional<at::Tensor> dres, at::Tensor dx,
+                 at::Tensor dw, bool accumulate) {
+  const int64_t H = h.size(-1);
+  const int64_t rows = h.numel() / H;
+  rows_check(dy, "dy", H);
+  rows_check(h, "h", H);
+  rows_check(dx, "dx", H);
+  TORCH_CHECK(dy.numel() == h.numel() && dx.numel() == h.numel(), "shape mismatch");
+  TORCH_CHECK(H % 8 == 0 && H <= 16384, "bad hidden size");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.is_contiguous() && dw.numel() == H, "dw must be fp32 [H]");
+  TORCH_CHECK(rstd.scalar_type() == at::kFloat && rstd.numel() == rows, "rstd must be fp32 [rows]");
+  const void* drp = nullptr;
+  if (dres.has_value()) {
+    rows_check(*dres, "dres", H);
+    TORCH_CHECK(dres->numel() == h.numel(), "dres shape mismatch");
+    drp = dres->data_ptr();
+  }
+  const int G = nxd::rmsnorm_bwd_num_partials(rows);
+  at::Tensor part = at::empty({(int64_t)G * H}, h.options().dtype(at::kFloat));
+  check_rc(nxd::rmsnorm_bwd_launch(dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), drp, dx.data_ptr(),
+                                   part.data_ptr<float>(), dw.data_ptr<float>(), accumulate ? 1 : 0, rows, (int)H, cur_stream()),
+           "rmsnorm_bwd");
+}
+
+void rope_inplace(at::Tensor buf, int64_t T, int64_t W, int64_t col0, int64_t nheads, int64_t D, at::Tensor cos_t,
+                  at::Tensor sin_t, c10::optional<at::Tensor> pos, int64_t pos_div, int64_t pos_mod, double sign) {
+  check_bf16(buf, "buf");
+  check_aligned16(buf, "buf");
+  TORCH_CHECK(D == 64 || D == 128 || D == 256, "rope head_dim must be 64/128/256");
+  TORCH_CHECK(W % 8 == 0 && col0 % 8 == 0, "rope row stride / column offset must be multiples of 8");
+  TORCH_CHECK(col0 + nheads * D <= W, "rope heads exceed the row");
+  TORCH_CHECK(buf.storage().nbytes() >= (size_t)((T - 1) * W + W) * 2 + buf.storage_offset() * 2 || T == 0,
+              "rope buffer too small");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
+                  sin_t.is_contiguous() && cos_t.size(-1) == D / 2 && sin_t.sizes() == cos_t.sizes(),
+              "cos/sin tables must be contiguous fp32 [max_pos, D/2]");
+  const int64_t* pp = nullptr;
+  if (pos.has_value()) {
+    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->is_contiguous() && pos->numel() == T, "pos must be int64 [T]");
+    pp = pos->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(pos_div > 0 && pos_mod > 0 && pos_mod <= cos_t.size(0), "bad implicit positions");
+  }
+  check_rc(nxd::rope_inplace_launch(buf.data_ptr(), T, W, (int)col0, (int)nheads, (int)D, cos_t.data_ptr<float>(),
+                                    sin_t.data_ptr<float>(), pp, pos_div, pos_mod, (float)sign, cur_stream()),
+           "rope");
+}
+
+void swiglu_fwd(at::Tensor gu, at::Tensor h) {
+  const int64_t I2 = gu.size(-1);
+  TORCH_CHECK(I2 % 16 == 0, "gate_up width must be a multiple of 16");
+  rows_check(gu, "gate_up", I2);
+  rows_check(h, "h", I2 / 2);
+  TORCH_CHECK(h.numel() * 2 == gu.numel(), "shape mismatch");
+  check_rc(nxd::swiglu_fwd_launch(gu.data_ptr(), h.data_ptr(), gu.numel() / I2, (int)(I2 / 2), cur_stream()), "swiglu_fwd");
+}
+
+void swiglu_bwd(at::Tensor gu, at::Tensor dh, at::Tensor dgu) {
+  const int64_t I2 = gu.size(-1);
+  TORCH_CHECK(I2 % 16 == 0, "gate_up width must be a multiple of 16");
+  rows_check(gu, "gate_up", I2);
+  rows_check(dh, "dh", I2 / 2);
+  rows_check(dgu, "dgu", I2);
+  TORCH_CHECK(dh.numel() * 2 == gu.numel() && dgu.numel() == gu.numel(), "shape mismatch");
+  check_rc(nxd::swiglu_bwd_launch(gu.data_ptr(), dh.data_ptr(), dgu.data_ptr(), gu.numel() / I2, (int)(I2 / 2), cur_stream()),
+           "swiglu_bwd");
+}
+
+void logits_check(const at::Tensor& x) {
+  check_cuda(x, "logits");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "logits must be [N, V] with unit column stride");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "logits must be bf16 or fp32");
+  TORCH_CHECK(x.size(1) % 8 == 0 && x.stride(0) % 8 == 0, "vocab shard and row stride must be multiples of 8");
+  check_aligned16(x, "logits");
+}
+
+void xent_stats(at::Tensor logits, at::Tensor labels, at::Tensor stats, int64_t vocab_start) {
+  logits_check(logits);
+  const int64_t N = logits.size(0);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == N, "labels must be int64 [N]");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.is_contiguous() && stats.numel() == N * 4, "stats must be fp32 [N,4]");
+  check_rc(nxd::xent_stats_launch(logits.data_ptr(), logits.scalar_type() == at::kFloat, labels.data_ptr<int64_t>(),
+                                  stats.data_ptr<float>(), N, (int)logits.size(1), logits.stride(0), vocab_start, cur_stream()),
+           "xent_stats");
+}
+
+void xent_bwd(at::Tensor logits, at::Tensor labels, at::Tensor gstat, at::Tensor grad, int64_t vocab_start, double eps,
+              int64_t vocab_total) {
+  logits_check(logits);
+  const int64_t N = logits.size(0);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == N, "labels must be int64 [N]");
+  TORCH_CHECK(gstat.scalar_type() == at::kFloat && gstat.is_contiguous() && gstat.numel() == N * 4, "gstat must be fp32 [N,4]");
+  check_bf16(grad, "grad");
+  TORCH_CHECK(grad.dim() == 2 && grad.size(0) == N && grad.size(1) == logits.size(1) && grad.stride(1) == 1 &&
+                  grad.stride(0) % 8 == 0,
+              "grad must be bf16 [N, V]");
+  check_aligned16(grad, "grad");
+  check_rc(nxd::xent_bwd_launch(logits.data_ptr(), logits.scalar_type() == at::kFloat, labels.data_ptr<int64_t>(),
+                                gstat.data_ptr<float>(), grad.data_ptr(), N, (int)logits.size(1), logits.stride(0),
+                                grad.stride(0), vocab_start, (float)eps, vocab_total, cur_stream()),
+           "xent_bwd");
+}
+
+void flat_check(const at::Tensor& t, const char* n) {
+  check_cuda(t, n);
+  TORCH_CHECK(t.is_contiguous(), n, " must be contiguous");
+  check_aligned16(t, n);
+}
+
+void flat_reduce(at::Tensor x, int64_t mode, at::Tensor out, bool accumulate) {
+  flat_check(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "x must be bf16/fp32");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 1, "out must be fp32");
+  TORCH_CHECK(mode == 0 || mode == 1, "mode must be 0 (sumsq) or 1 (max abs)");
+  at::Tensor part = at::empty({2048}, x.options().dtype(at::kFloat));
+  check_rc(nxd::flat_reduce_launch(x.data_ptr(), x.scalar_type() == at::kBFloat16, x.numel(), (int)mode, part.data_ptr<float>(),
+                                   out.data_ptr<float>(), accumulate ? 1 : 0, cur_stream()),
+           "flat_reduce");
+}
+
+void adamw_flat(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, c10::optional<at::Tensor> p16, double lr, double b1,
+                double b2, double eps, double wd, double bc1, double bc2, c10::optional<at::Tensor> gscale, double gscale_host) {
+  flat_check(p, "p");
+  flat_check(g, "g");
+  flat_check(m, "m");
+  flat_check(v, "v");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
+              "p/m/v must be fp32");
+  TORCH_CHECK(g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16, "g must be fp32/bf16");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "size mismatch");
+  void* o = nullptr;
+  if (p16.has_value()) {
+    flat_check(*p16, "p16");
+    TORCH_CHECK(p16->scalar_type() == at::kBFloat16 && p16->numel() == n, "p16 must be bf16 of the same size");
+    o = p16->data_ptr();
+  }
+  const float* gs = nullptr;
+  if (gscale.has_value()) {
+    TORCH_CHECK(gscale->scalar_type() == at::kFloat && gscale->is_cuda(), "gscale must be a fp32 GPU tensor");
+    gs = gscale->data_ptr<float>();
+  }
+  check_rc(nxd::adamw_flat_launch(p.data_ptr<float>(), g.data_ptr(), g.scalar_type() == at::kBFloat16, m.data_ptr<float>(),
+                                  v.data_ptr<float>(), o, n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1,
+                                  (float)bc2, gs, (float)gscale_host, cur_stream()),
+           "adamw_flat");
+}
+
+void clip_coef(at::Tensor stat, at::Tensor coef, double max_norm, bool is_sumsq) {
+  TORCH_CHECK(stat.scalar_type() == at::kFloat && coef.scalar_type() == at::kFloat && coef.numel() >= 2 && stat.is_cuda(),
+              "clip_coef: fp32 GPU tensors, coef of size >= 2");
+  check_rc(nxd::clip_coef_launch(stat.data_ptr<float>(), coef.data_ptr<float>(), (float)max_norm, is_sumsq ? 1 : 0, cur_stream()),
+           "clip_coef");
+}
+
+void scale_flat(at::Tensor x, at::Tensor s) {
+  flat_check(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && s.scalar_type() == at::kFloat && s.is_cuda(), "fp32 tensors required");
+  check_rc(nxd::scale_flat_launch(x.data_ptr<float>(), x.numel(), s.data_ptr<float>(), cur_stream()), "scale_flat");
+}
+
+void embedding_fwd(at::Tensor ids, at::Tensor w, at::Tensor out, int64_t start) {
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.is_cuda(), "ids must be int64 contiguous");
+  check_bf16(w, "w");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w must be contiguous [V, H]");
+  const int64_t H = w.size(1);
+  TORCH_CHECK(H % 8 == 0, "embedding dim must be a multiple of 8");
+  rows_check(out, "out", H);
+  TORCH_CHECK(out.numel() == ids.numel() * H, "out shape mismatch");
+  check_aligned16(w, "w");
+  check_rc(nxd::embedding_fwd_launch(ids.data_ptr<int64_t>(), w.data_ptr(), out.data_ptr(), ids.numel(), (int)H, start,
+                                     w.size(0), cur_stream()),
+           "embedding_fwd");
+}
+
+void embedding_bwd(at::Tensor ids, at::Tensor dout, at::Tensor dw, int64_t start) {
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.is_cuda(), "ids must be int64 contiguous");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.dim() == 2 && dw.is_contiguous(), "dw must be fp32 [V, H]");
+  const int64_t H = dw.size(1);
+  rows_check(dout, "dout", H);
+  TORCH_CHECK(dout.numel() == ids.numel() * H, "dout shape mismatch");
+  check_rc(nxd::embedding_bwd_launch(ids.data_ptr<int64_t>(), dout.data_ptr(), dw.data_ptr<float>(), ids.numel(), (int)H,
+                                     start, dw.size(0), cur_stream()),
+           "embedding_bwd");
+}
+
+// q: [B, T, Hq, D] (strided), caches: [Bc, Hkv, Lmax, D] contiguous, out: [B, T, Hq, D]
+void decode_attn(at::Tensor q, at::Tensor kc, at::Tensor vc, c10::optional<at::Tensor> cache_idx, at::Tensor seq_len,
+                 at::Tensor out, double scale, int64_t nsplit) {
+  int64_t qs[3], os[3];
+  bshd_strides(q, "q", qs);
+  bshd_strides(out, "out", os);
+  check_bf16(kc, "k_cache");
+  check_bf16(vc, "v_cache");
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.sizes() == kc.sizes() && vc.is_contiguous(),
+              "caches must be contiguous [B, Hkv, Lmax, D]");
+  const int B = q.size(0), T = q.size(1), Hq = q.size(2), D = q.size(3);
+  const int Hkv = kc.size(1), Lmax = kc.size(2);
+  TORCH_CHECK(kc.size(3) == D && (D == 64 || D == 128), "head dim mismatch (64/128)");
+  TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0, "q heads must be a multiple of kv heads");
+  TORCH_CHECK((int64_t)(Hq / Hkv) * T <= 64, "decode supports (Hq/Hkv) * new_tokens <= 64");
+  TORCH_CHECK(nsplit >= 1 && nsplit * 128 >= Lmax, "nsplit * 128 must cover the cache length");
+  TORCH_CHECK(seq_len.scalar_type() == at::kInt && seq_len.numel() == B && seq_len.is_contiguous(), "seq_len must be int32 [B]");
+  const int* ci = nullptr;
+  if (cache_idx.has_value()) {
+    TORCH_CHECK(cache_idx->scalar_type() == at::kInt && cache_idx->numel() == B, "cache_idx must be int32 [B]");
+    ci = cache_idx->data_ptr<int>();
+  } else {
+    TORCH_CHECK(kc.size(0) >= B, "cache batch too small");
+  }
+  TORCH_CHECK(out.sizes() == q.sizes(), "out shape mismatch");
+  const int M = (Hq / Hkv) * T;
+  auto opts = q.options().dtype(at::kFloat);
+  at::Tensor po = at::empty({(int64_t)B * Hkv * nsplit * M * D}, opts);
+  at::Tensor pm = at::empty({(int64_t)B * Hkv * nsplit * M}, opts);
+  at::Tensor pl = at::empty({(int64_t)B * Hkv * nsplit * M}, opts);
+  const int64_t cs[3] = {kc.stride(0), kc.stride(1), kc.stride(2)};
+  (void)Lmax;
+  check_rc(nxd::decode_attn_launch(q.data_ptr(), qs, kc.data_ptr(), vc.data_ptr(), cs, ci, seq_len.data_ptr<int>(),
+                                   po.data_ptr<float>(), pm.data_ptr<float>(), pl.data_ptr<float>(), out.data_ptr(), os, B, T,
+                                   Hq, Hkv, D, (int)nsplit, (float)scale, cur_stream()),
+           "decode_attn");
+}
+
+// k, v: [B, T, Hkv, D] strided; caches [Bc, Hkv, Lmax, D]; pos: int32 [B] position of token 0
+void kv_cache_write(at::Tensor k, at::Tensor v, at::Tensor kc, at::Tensor vc, c10::optional<at::Tensor> cache_idx,
+                    at::Tensor pos) {
+  int64_t ks[3], vs[3];
+  bshd_strides(k, "k", ks);
+  bshd_strides(v, "v", vs);
+  TORCH_CHECK(ks[0] == vs[0] && ks[1] == vs[1] && ks[2] == vs[2] && k.sizes() == v.sizes(), "k/v layouts must match");
+  check_bf16(kc, "k_cache");
+  check_bf16(vc, "v_cache");
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.sizes() == kc.sizes() && vc.is_contiguous(), "bad caches");
+  const int B = k.size(0), T = k.size(1), H = k.size(2), D = k.size(3);
+  TORCH_CHECK(kc.size(1) == H && kc.size(3) == D && D % 8 == 0, "cache / new kv mismatch");
+  TORCH_CHECK(pos.scalar_type() == at::kInt && pos.numel() == B, "pos must be int32 [B]");
+  const int* ci = nullptr;
+  if (cache_idx.has_value()) {
+    TORCH_CHECK(cache_idx->scalar_type() == at::kInt && cache_idx->numel() == B, "cache_idx must be int32 [B]");
+    ci = cache_idx->data_ptr<int>();
+  } else {
+    TORCH_CHECK(kc.size(0) >= B, "cache batch too small");
+  }
+  const int64_t cs[3] = {kc.stride(0), kc.stride(1), kc.stride(2)};
+  check_rc(nxd::kv_cache_write_launch(k.data_ptr(), v.data_ptr(), ks, kc.data_ptr(), vc.data_ptr(), cs, ci, pos.data_ptr<int>(),
+                                      B, T, H, D, (int)kc.size(2), cur_stream()),
+           "kv_cache_write");
+}
+
+void argmax_rows(at::Tensor x, at::Tensor out) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [B, V]");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be fp32/bf16");
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() == x.size(0), "out must be int64 [B]");
+  check_rc(nxd::argmax_launch(x.data_ptr(), x.scalar_type() == at::kFloat, x.stride(0), (int)x.size(0), (int)x.size(1),
+                              out.data_ptr<int64_t>(), cur_stream()),
+           "argmax");
+}
+
+void topk_sample(at::Tensor x, int64_t k, double temperature, c10::optional<at::Tensor> uniform, at::Tensor out,
+                 c10::optional<at::Tensor> vals, c10::optional<at::Tensor> idx) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [B, V]");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be fp32/bf16");
+  const int64_t B = x.size(0);
+  TORCH_CHECK(k >= 1 && k <= 1024 && k <= x.size(1), "top_k must be in [1, 1024]");
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() == B, "out must be int64 [B]");
+  const float* u = nullptr;
+  if (uniform.has_value()) {
+    TORCH_CHECK(uniform->scalar_type() == at::kFloat && uniform->numel() == B, "uniform must be fp32 [B]");
+    u = uniform->data_ptr<float>();
+  }
+  float* vp = nullptr;
+  int64_t* ip = nullptr;
+  if (vals.has_value()) {
+    TORCH_CHECK(vals->scalar_type() == at::kFloat && vals->numel() == B * k, "vals must be fp32 [B, k]");
+    vp = vals->data_ptr<float>();
+  }
+  if (idx.has_value()) {
+    TORCH_CHECK(idx->scalar_type() == at::kLong && idx->numel() == B * k, "idx must be int64 [B, k]");
+    ip = idx->data_ptr<int64_t>();
+  }
+  check_rc(nxd::topk_sample_launch(x.data_ptr(), x.scalar_type() == at::kFloat, x.stride(0), (int)B, (int)x.size(1), (int)k,
+                                   (float)temperature, u, out.data_ptr<int64_t>(), vp, ip, cur_stream()),
+           "topk_sample");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "CDNA4 (gfx950) kernels of neuronx_distributed_llama3_2_amd";
+  m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rope_inplace", &rope_inplace);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("xent_stats", &xent_stats);
+  m.def("xent_bwd", &xent_bwd);
+  m.def("flat_reduce", &flat_reduce);
+  m.def("adamw_flat", &adamw_flat);
+  m.def("clip_coef", &clip_coef);
+  m.def("scale_flat", &scale_flat);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.def("decode_attn", &decode_attn);
+  m.def("kv_cache_write", &kv_cache_write);
+  m.def("argmax_rows", &argmax_rows);
+  m.def("topk_sample", &topk_sample);
+  m.attr("ARCH") = "gfx950";
+}

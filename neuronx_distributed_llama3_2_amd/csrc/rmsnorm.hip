@@ -1,0 +1,184 @@
+// RMSNorm forward / backward for CDNA4, optionally fused with the residual add of a pre-norm
+// transformer block.  Replaces the reference's fp64 LlamaRMSNorm
+// (examples/training/llama/modeling_llama_nxd.py:134-149) and the inference RmsNorm custom call
+// (examples/inference/modules/custom_calls.py:5-16).
+//
+//   fwd:  h = x (+ residual);  y = h * rsqrt(mean(h^2) + eps) * w        (bf16 io, fp32 math)
+//   bwd:  dh = rstd * (dy*w - xhat * mean(dy*w*xhat)) (+ dres);  dw = sum_rows dy * xhat
+//
+// Memory-bound: one row per workgroup, 16-byte vector loads (Guideline 13), the row stays in
+// registers between the reduction and the normalisation (no re-read).  dw partials are written
+// per workgroup ([G, H] fp32) and summed by a column-reduction kernel (no float atomics, so the
+// result is bitwise reproducible).
+#include "common.h"
+
+namespace nxd {
+namespace rms {
+
+template <int VPT>  // 8-element vectors per thread
+__global__ void __launch_bounds__(256) fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+                                                  const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                                                  uint16_t* __restrict__ h_out, float* __restrict__ rstd_out,
+                                                  int64_t rows, int H, float eps) {
+  __shared__ float red[16];
+  const int64_t row = blockIdx.x;
+  if (row >= rows) return;
+  const int nvec = H / 8;
+  const uint16_t* xr = x + row * H;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nvec) {
+      u32x4_t xv = *reinterpret_cast<const u32x4_t*>(xr + c * 8);
+      unpack8(xv, v[i]);
+      if (res) {
+        float rv[8];
+        unpack8(*reinterpret_cast<const u32x4_t*>(res + row * H + c * 8), rv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = bf2f(f2bf(v[i][j] + rv[j]));  // round like the stored h
+        *reinterpret_cast<u32x4_t*>(h_out + row * H + c * 8) = pack8(v[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  const float tot = block_sum(ss, red);
+  const float rstd = rsqrtf(tot / (float)H + eps);
+  if (threadIdx.x == 0 && rstd_out) rstd_out[row] = rstd;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nvec) {
+      float wv[8], o[8];
+      unpack8(*reinterpret_cast<const u32x4_t*>(w + c * 8), wv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * rstd * wv[j];
+      *reinterpret_cast<u32x4_t*>(y + row * H + c * 8) = pack8(o);
+    }
+  }
+}
+
+// grid-stride over rows; each workgroup accumulates its dw partial in registers.
+template <int VPT>
+__global__ void __launch_bounds__(256) bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ h,
+                                                  const uint16_t* __restrict__ w, const float* __restrict__ rstd,
+                                                  const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
+                                                  float* __restrict__ dw_part, int64_t rows, int H) {
+  __shared__ float red[16];
+  const int nvec = H / 8;
+  float wv[VPT][8], dwa[VPT][8];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dwa[i][j] = 0.f;
+    if (c < nvec) unpack8(*reinterpret_cast<const u32x4_t*>(w + c * 8), wv[i]);
+  }
+  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    const float rs = rstd[row];
+    float xh[VPT][8], g[VPT][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * blockDim.x;
+      if (c < nvec) {
+        float hv[8], dv[8];
+        unpack8(*reinterpret_cast<const u32x4_t*>(h + row * H + c * 8), hv);
+        unpack8(*reinterpret_cast<const u32x4_t*>(dy + row * H + c * 8), dv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[i][j] = hv[j] * rs;
+          g[i][j] = dv[j] * wv[i][j];
+          dot += g[i][j] * xh[i][j];
+          dwa[i][j] += dv[j] * xh[i][j];
+        }
+      }
+    }
+    const float mean = block_sum(dot, red) / (float)H;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * blockDim.x;
+      if (c < nvec) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs * (g[i][j] - xh[i][j] * mean);
+        if (dres) {
+          float rv[8];
+          unpack8(*reinterpret_cast<const u32x4_t*>(dres + row * H + c * 8), rv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += rv[j];
+        }
+        *reinterpret_cast<u32x4_t*>(dx + row * H + c * 8) = pack8(o);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nvec) {
+      float* dst = dw_part + (int64_t)blockIdx.x * H + c * 8;
+      *reinterpret_cast<f32x4_t*>(dst) = f32x4_t{dwa[i][0], dwa[i][1], dwa[i][2], dwa[i][3]};
+      *reinterpret_cast<f32x4_t*>(dst + 4) = f32x4_t{dwa[i][4], dwa[i][5], dwa[i][6], dwa[i][7]};
+    }
+  }
+}
+
+// dw[c] = sum_g part[g][c]  (fp32 out; optionally accumulated into an fp32 main_grad)
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, float* __restrict__ out, int G, int H,
+                                                    int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= H) return;
+  float s = 0.f;
+  for (int gi = 0; gi < G; ++gi) s += part[(int64_t)gi * H + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+}  // namespace rms
+
+int rmsnorm_fwd_launch(const void* x, const void* res, const void* w, void* y, void* h_out, float* rstd, int64_t rows,
+                       int H, float eps, hipStream_t stream) {
+  using namespace rms;
+  if (H % 8 != 0) return -1;
+  const int nvec = H / 8;
+  const int threads = nvec >= 256 ? 256 : ((nvec + 63) / 64) * 64;
+  const int vpt = (nvec + threads - 1) / threads;
+  const dim3 grid((unsigned)rows), block(threads);
+#define RMS_FWD(V) hipLaunchKernelGGL(fwd_kernel<V>, grid, block, 0, stream, (const uint16_t*)x, (const uint16_t*)res, \
+                                      (const uint16_t*)w, (uint16_t*)y, (uint16_t*)h_out, rstd, rows, H, eps)
+  if (vpt <= 1) RMS_FWD(1);
+  else if (vpt <= 2) RMS_FWD(2);
+  else if (vpt <= 4) RMS_FWD(4);
+  else if (vpt <= 8) RMS_FWD(8);
+  else return -2;
+#undef RMS_FWD
+  return (int)hipGetLastError();
+}
+
+// dw_part must hold G*H floats where G = rmsnorm_bwd_num_partials(rows)
+int rmsnorm_bwd_num_partials(int64_t rows) { return (int)(rows < 512 ? rows : 512); }
+
+int rmsnorm_bwd_launch(const void* dy, const void* h, const void* w, const float* rstd, const void* dres, void* dx,
+                       float* dw_part, float* dw, int accumulate_dw, int64_t rows, int H, hipStream_t stream) {
+  using namespace rms;
+  if (H % 8 != 0) return -1;
+  const int nvec = H / 8;
+  const int threads = nvec >= 256 ? 256 : ((nvec + 63) / 64) * 64;
+  const int vpt = (nvec + threads - 1) / threads;
+  const int G = rmsnorm_bwd_num_partials(rows);
+  if (G == 0) return 0;
+  const dim3 grid(G), block(threads);
+#define RMS_BWD(V) hipLaunchKernelGGL(bwd_kernel<V>, grid, block, 0, stream, (const uint16_t*)dy, (const uint16_t*)h, \
+                                      (const uint16_t*)w, rstd, (const uint16_t*)dres, (uint16_t*)dx, dw_part, rows, H)
+  if (vpt <= 1) RMS_BWD(1);
+  else if (vpt <= 2) RMS_BWD(2);
+  else if (vpt <= 4) RMS_BWD(4);
+  else if (vpt <= 8) RMS_BWD(8);
+  else return -2;
+#undef RMS_BWD
+  hipLaunchKernelGGL(colsum_kernel, dim3((H + 255) / 256), dim3(256), 0, stream, dw_part, dw, G, H, accumulate_dw);
+  return (int)hipGetLastError();
+}
+
+}  // namespace nxd

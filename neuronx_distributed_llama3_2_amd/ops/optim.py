@@ -1,0 +1,92 @@
+"""Flat-buffer optimizer primitives (csrc/optim.hip): multi-tensor grad norm, on-device clip
+coefficient and a fused AdamW with fp32 master weights + bf16 copy-out.
+
+All functions accept either GPU tensors (HIP kernels) or CPU tensors (torch reference), so the
+optimizer logic above them is the same on both.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ._ext import ext, use_native
+
+
+def flat_sumsq(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """out[0] (+)= sum(x^2) in fp32 for a contiguous flat buffer."""
+    if out is None:
+        out = torch.zeros(1, dtype=torch.float32, device=x.device)
+    if x.numel() == 0:
+        if not accumulate:
+            out.zero_()
+        return out
+    if use_native(x):
+        ext().flat_reduce(x.contiguous().view(-1), 0, out, accumulate)
+        return out
+    v = x.float().pow(2).sum()
+    if accumulate:
+        out += v
+    else:
+        out.fill_(float(v))
+    return out
+
+
+def flat_absmax(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    if out is None:
+        out = torch.zeros(1, dtype=torch.float32, device=x.device)
+    if x.numel() == 0:
+        if not accumulate:
+            out.zero_()
+        return out
+    if use_native(x):
+        ext().flat_reduce(x.contiguous().view(-1), 1, out, accumulate)
+        return out
+    v = x.float().abs().max()
+    if accumulate:
+        torch.maximum(out, v.reshape(1), out=out)
+    else:
+        out.fill_(float(v))
+    return out
+
+
+def clip_coefficient(stat: torch.Tensor, max_norm: float, is_sumsq: bool = True) -> torch.Tensor:
+    """Device tensor [coef, norm] with coef = min(1, max_norm / (norm + 1e-6))."""
+    coef = torch.empty(2, dtype=torch.float32, device=stat.device)
+    if use_native(stat):
+        ext().clip_coef(stat, coef, float(max_norm), bool(is_sumsq))
+        return coef
+    norm = stat[0].sqrt() if is_sumsq else stat[0]
+    coef[0] = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+    coef[1] = norm
+    return coef
+
+
+def adamw_flat_(p32: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
+                p16: Optional[torch.Tensor], lr: float, beta1: float, beta2: float, eps: float, weight_decay: float,
+                step: int, grad_scale: Optional[torch.Tensor] = None, grad_scale_host: float = 1.0,
+                bias_correction: bool = True) -> None:
+    """In-place AdamW (decoupled weight decay) over flat fp32 buffers; writes bf16 params to p16."""
+    bc1 = 1.0 - beta1 ** step if bias_correction else 1.0
+    bc2 = 1.0 - beta2 ** step if bias_correction else 1.0
+    if use_native(p32, grad):
+        ext().adamw_flat(p32, grad, exp_avg, exp_avg_sq, p16, lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale,
+                         grad_scale_host)
+        return
+    g = grad.float() * grad_scale_host
+    if grad_scale is not None:
+        g = g * grad_scale[0]
+    exp_avg.mul_(beta1).add_(g, alpha=1 - beta1)
+    exp_avg_sq.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    denom = exp_avg_sq.sqrt() / (bc2 ** 0.5) + eps
+    p32.mul_(1 - lr * weight_decay).addcdiv_(exp_avg, denom, value=-lr / bc1)
+    if p16 is not None:
+        p16.copy_(p32)
+
+
+def scale_flat_(x: torch.Tensor, s: torch.Tensor) -> None:
+    if use_native(x):
+        ext().scale_flat(x, s)
+    else:
+        x.mul_(s[0])

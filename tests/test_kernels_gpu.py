@@ -1,0 +1,242 @@
+"""Numerics of every hand-written HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Runs only on an MI355X (marker `gpu`).  Each test also asserts that the native extension is the
+code path in use (no silent fallback).
+"""
+
+import math
+
+import pytest
+import torch
+
+import neuronx_distributed_llama3_2_amd.ops as ops
+from neuronx_distributed_llama3_2_amd.ops import _ext
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+@pytest.fixture(autouse=True)
+def _native():
+    assert _ext.ext_available(), "HIP extension must be built for GPU tests"
+    torch.manual_seed(0)
+    yield
+
+
+def _attn_inputs(B, Sq, Sk, Hq, Hkv, D, layout="bshd"):
+    q = torch.randn(B, Sq, Hq, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    return q, k, v
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("S", [128, 333, 1024])
+def test_flash_fwd(D, causal, S):
+    B, Hq, Hkv = 2, 8, 2
+    q, k, v = _attn_inputs(B, S, S, Hq, Hkv, D)
+    o, lse = ops.flash_attn_fwd_lse(q, k, v, causal=causal)
+    ro, rlse = ops.attention_reference(q, k, v, causal=causal)
+    assert (o.float() - ro).abs().max().item() < 2e-2
+    assert (lse - rlse).abs().max().item() < 1e-2
+
+
+def test_flash_fwd_forced_rescale():
+    # rule 26: force the online-softmax max to jump late in the key sweep
+    B, S, Hq, Hkv, D = 1, 512, 4, 1, 128
+    q, k, v = _attn_inputs(B, S, S, Hq, Hkv, D)
+    k[:, 400] = q[:, 450, 0] * 4  # spike key 400 against query 450
+    o, lse = ops.flash_attn_fwd_lse(q, k, v, causal=True)
+    ro, rlse = ops.attention_reference(q, k, v, causal=True)
+    assert (o.float() - ro).abs().max().item() < 3e-2
+    assert (lse - rlse).abs().max().item() < 2e-2
+
+
+def test_flash_fwd_cross_lengths():
+    B, Sq, Sk, Hq, Hkv, D = 2, 100, 300, 8, 8, 64
+    q, k, v = _attn_inputs(B, Sq, Sk, Hq, Hkv, D)
+    o, lse = ops.flash_attn_fwd_lse(q, k, v, causal=True)  # bottom-right aligned
+    ro, rlse = ops.attention_reference(q, k, v, causal=True)
+    assert (o.float() - ro).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("S", [128, 257, 1024])
+def test_flash_bwd(D, causal, S):
+    B, Hq, Hkv = 2, 8, 2
+    q, k, v = _attn_inputs(B, S, S, Hq, Hkv, D)
+    q.requires_grad_(True)
+    k.requires_grad_(True)
+    v.requires_grad_(True)
+    o = ops.flash_attn_func(q, k, v, causal=causal)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qf, kf, vf = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ro, _ = ops.attention_reference(qf, kf, vf, causal=causal)
+    ro.backward(do.float())
+    assert _rel(q.grad, qf.grad) < 2e-2
+    assert _rel(k.grad, kf.grad) < 2e-2
+    assert _rel(v.grad, vf.grad) < 2e-2
+
+
+def test_rope_attention_fused_qkv():
+    S, B, nq, nkv, D = 256, 2, 8, 2, 128
+    W = (nq + 2 * nkv) * D
+    inv = ops.llama3_inv_freq(D, 500000.0, 8.0, 1.0, 4.0, 8192)
+    cos_t, sin_t = ops.rope_tables(inv, 1024, device=DEV)
+    qkv0 = torch.randn(S, B, W, device=DEV, dtype=torch.bfloat16)
+    qkv = qkv0.clone().requires_grad_(True)
+    o = ops.rope_attention(qkv.clone(), cos_t, sin_t, nq, nkv, D)
+    # reference on the CPU path (plain torch ops)
+    qr = qkv0.detach().cpu().float().requires_grad_(True)
+    ro = ops.rope_attention(qr, cos_t.cpu(), sin_t.cpu(), nq, nkv, D)
+    assert _rel(o.cpu(), ro) < 2e-2
+    do = torch.randn_like(o)
+    o.backward(do)
+    ro.backward(do.cpu().float())
+    assert _rel(qkv.grad.cpu(), qr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("H", [2048, 4096, 8192])
+def test_rmsnorm(H):
+    x = torch.randn(37, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(37, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    y, h = ops.rms_norm(x, w, 1e-5, residual=r)
+    xf, rf, wf = (t.detach().float().requires_grad_(True) for t in (x, r, w))
+    hf = xf + rf
+    yf = ops.rms_norm_reference(hf, wf, 1e-5)
+    assert _rel(y, yf) < 1e-2
+    assert _rel(h, hf) < 1e-2
+    dy = torch.randn_like(y)
+    dh = torch.randn_like(h)
+    (y.float() * dy.float()).sum().add((h.float() * dh.float()).sum()).backward()
+    (yf * dy.float()).sum().add((hf * dh.float()).sum()).backward()
+    assert _rel(x.grad, xf.grad) < 2e-2
+    assert _rel(r.grad, rf.grad) < 2e-2
+    assert _rel(w.grad, wf.grad) < 2e-2
+
+
+def test_rope_inplace():
+    T, nh, D = 64, 6, 128
+    W = nh * D + 256
+    buf = torch.randn(T, W, device=DEV, dtype=torch.bfloat16)
+    ref = buf.clone().cpu().float()
+    inv = ops.llama3_inv_freq(D, 10000.0)
+    c, s = ops.rope_tables(inv, 128, device=DEV)
+    pos = torch.randint(0, 128, (T,), device=DEV)
+    ops.rope_inplace_(buf, 0, nh, D, c, s, pos)
+    x = ref[:, : nh * D].view(T, nh, D)
+    out = ops.apply_rotary_reference(x, c.cpu(), s.cpu(), pos.cpu())
+    assert _rel(buf[:, : nh * D].cpu().view(T, nh, D), out) < 1e-2
+    assert torch.equal(buf[:, nh * D:].cpu().float(), ref[:, nh * D:])
+    ops.rope_inplace_(buf, 0, nh, D, c, s, pos, sign=-1.0)
+    assert _rel(buf[:, : nh * D].cpu(), ref[:, : nh * D]) < 2e-2
+
+
+def test_swiglu():
+    gu = torch.randn(65, 2 * 1792, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    h = ops.swiglu(gu)
+    gf = gu.detach().float().requires_grad_(True)
+    hf = ops.swiglu_reference(gf)
+    assert _rel(h, hf) < 1e-2
+    dh = torch.randn_like(h)
+    h.backward(dh)
+    hf.backward(dh.float())
+    assert _rel(gu.grad, gf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("smooth", [0.0, 0.1])
+def test_cross_entropy(dtype, smooth):
+    N, V = 77, 16032
+    logits = (3 * torch.randn(N, V, device=DEV)).to(dtype).requires_grad_(True)
+    labels = torch.randint(0, V, (N,), device=DEV)
+    labels[5] = -100
+    loss = ops.vocab_parallel_cross_entropy(logits, labels, label_smoothing=smooth)
+    lf = logits.detach().float().requires_grad_(True)
+    rl = ops.parallel_cross_entropy_reference(lf, labels, label_smoothing=smooth)
+    assert (loss - rl).abs().max().item() < 1e-3 * max(1.0, rl.abs().max().item())
+    g = torch.rand(N, device=DEV)
+    loss.backward(g)
+    rl.backward(g)
+    assert _rel(logits.grad, lf.grad) < 2e-2
+
+
+def test_embedding():
+    V, H, T = 1000, 512, 300
+    w = torch.randn(V, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    ids = torch.randint(0, 2 * V, (3, T // 3), device=DEV)
+    out = ops.vocab_parallel_embedding(ids, w, vocab_start=V // 2)
+    local = ids - V // 2
+    mask = (local >= 0) & (local < V)
+    ref = w.detach()[local.clamp(0, V - 1)] * mask[..., None]
+    assert torch.equal(out, ref)
+    d = torch.randn_like(out)
+    out.backward(d)
+    refg = torch.zeros(V, H, device=DEV)
+    refg.index_add_(0, local.clamp(0, V - 1).view(-1), (d.float() * mask[..., None]).view(-1, H))
+    assert _rel(w.grad, refg) < 1e-2
+
+
+def test_flat_reduce_and_adamw():
+    n = 1_000_003
+    g = torch.randn(n, device=DEV, dtype=torch.bfloat16)
+    s = ops.flat_sumsq(g)
+    assert abs(s.item() - g.float().pow(2).sum().item()) / s.item() < 1e-4
+    mx = ops.flat_absmax(g)
+    assert mx.item() == g.float().abs().max().item()
+    p = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    p16 = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    pr, mr, vr = p.clone().cpu(), m.clone().cpu(), v.clone().cpu()
+    coef = ops.clip_coefficient(s, 1.0)
+    for step in (1, 2):
+        ops.adamw_flat_(p, g, m, v, p16, 1e-3, 0.9, 0.95, 1e-8, 0.1, step, grad_scale=coef)
+        ops.adamw_flat_(pr, g.cpu(), mr, vr, None, 1e-3, 0.9, 0.95, 1e-8, 0.1, step, grad_scale=coef.cpu())
+    assert _rel(p.cpu(), pr) < 1e-5
+    assert torch.equal(p16.cpu(), p.cpu().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_decode_attention_and_cache(D):
+    B, Hq, Hkv, L, T = 3, 32, 8, 700, 2
+    kc = torch.zeros(B, Hkv, L, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    kc[:, :, :600] = torch.randn(B, Hkv, 600, D, device=DEV, dtype=torch.bfloat16)
+    vc[:, :, :600] = torch.randn(B, Hkv, 600, D, device=DEV, dtype=torch.bfloat16)
+    knew = torch.randn(B, T, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    vnew = torch.randn(B, T, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.tensor([100, 333, 598], device=DEV, dtype=torch.int32)
+    ops.kv_cache_write(knew, vnew, kc, vc, pos)
+    for b in range(B):
+        assert torch.equal(kc[b, :, pos[b]:pos[b] + T], knew[b].transpose(0, 1))
+    q = torch.randn(B, T, Hq, D, device=DEV, dtype=torch.bfloat16)
+    seq = pos + T
+    o = ops.decode_attention(q, kc, vc, seq)
+    kc_c, vc_c = kc.cpu(), vc.cpu()
+    ro = ops.decode_attention(q.cpu(), kc_c, vc_c, seq.cpu())
+    assert _rel(o.cpu(), ro) < 2e-2
+
+
+def test_sampling():
+    B, V = 4, 128256
+    x = torch.randn(B, V, device=DEV)
+    assert torch.equal(ops.argmax_rows(x), torch.argmax(x, -1))
+    u = torch.rand(B, device=DEV)
+    tok, vals, idx = ops.topk_sample(x, 50, 1.0, u, return_topk=True)
+    rv, ri = torch.topk(x, 50, -1)
+    assert torch.allclose(vals, rv)
+    assert torch.equal(idx, ri)
+    rt = ops.topk_sample(x.cpu(), 50, 1.0, u.cpu())
+    assert torch.equal(tok.cpu(), rt)
