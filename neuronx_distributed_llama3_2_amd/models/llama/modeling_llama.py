@@ -1,0 +1,247 @@
+"""Llama-2/3/3.1/3.2 causal LM for tensor + sequence parallel training on MI355X.
+
+Capability parity with the reference training model (examples/training/llama/modeling_llama_nxd.py:134-774):
+GQA QKV column-parallel projection with KV replication, fused gate_up (stride=2) / down MLP,
+vocab-parallel embedding + lm_head + cross entropy, Megatron sequence parallelism, flash
+attention, selective / full activation checkpointing.  MI355X-first structure:
+
+* activations are [S, B, H] (sequence-major) so the SP shard of a rank is one contiguous slab;
+* each decoder block is: fused (residual add + RMSNorm) kernel -> ONE QKV GEMM into a fused
+  buffer -> in-place RoPE + GQA flash attention on strided views of that buffer (no transposes,
+  no repeat_kv) -> o_proj (reduce-scatter) -> fused add+norm -> gate_up GEMM -> SwiGLU kernel ->
+  down GEMM (reduce-scatter);
+* the embedding reduce-scatters straight into the SP layout and the lm_head all-gathers from it
+  (one collective each way), the loss is the fused vocab-parallel cross entropy whose backward
+  overwrites the logits buffer in place; no fp64 anywhere (the reference upcasts logits and norms
+  to fp64 only to survive XLA_DOWNCAST_BF16).
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from functools import partial
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+from torch.utils.checkpoint import checkpoint
+
+from ... import ops
+from ...modules.qkv_linear import GQAQKVColumnParallelLinear
+from ...parallel_layers.layer_norm import RMSNorm
+from ...parallel_layers.layers import ColumnParallelLinear, ParallelEmbedding, RowParallelLinear
+from ...parallel_layers.loss_functions import parallel_cross_entropy
+from ...parallel_layers.mappings import gather_from_sequence_parallel_region, scatter_to_sequence_parallel_region
+from ...parallel_layers.parallel_state import get_tensor_model_parallel_size
+from ...parallel_layers.utils import divide
+
+
+@dataclass
+class CausalLMOutput:
+    loss: Optional[torch.Tensor] = None
+    logits: Optional[torch.Tensor] = None
+
+    def __getitem__(self, i):
+        return (self.loss, self.logits)[i] if self.loss is not None else (self.logits,)[i]
+
+
+def _init_normal(std, w):
+    return nn.init.normal_(w, mean=0.0, std=std)
+
+
+class LlamaMLP(nn.Module):
+    def __init__(self, config, dtype, device):
+        super().__init__()
+        sp = getattr(config, "sequence_parallel_enabled", False)
+        init = partial(_init_normal, config.initializer_range)
+        self.gate_up_proj = ColumnParallelLinear(config.hidden_size, 2 * config.intermediate_size, stride=2, bias=False,
+                                                 gather_output=False, init_method=init, sequence_parallel_enabled=sp,
+                                                 dtype=dtype, device=device)
+        self.down_proj = RowParallelLinear(config.intermediate_size, config.hidden_size, bias=False,
+                                           input_is_parallel=True, init_method=init, sequence_parallel_enabled=sp,
+                                           dtype=dtype, device=device)
+        self.selective_checkpoint = getattr(config, "selective_checkpoint_enabled", False)
+
+    def forward(self, x):
+        gu = self.gate_up_proj(x)
+        if self.selective_checkpoint and self.training:
+            h = checkpoint(ops.swiglu, gu, use_reentrant=False)
+        else:
+            h = ops.swiglu(gu)
+        return self.down_proj(h)
+
+
+class LlamaAttention(nn.Module):
+    def __init__(self, config, dtype, device, rope_cache):
+        super().__init__()
+        self.config = config
+        self.hidden_size = config.hidden_size
+        self.num_heads = config.num_attention_heads
+        self.num_kv_heads = getattr(config, "num_key_value_heads", None) or self.num_heads
+        self.head_dim = getattr(config, "head_dim", None) or self.hidden_size // self.num_heads
+        tp = get_tensor_model_parallel_size()
+        kv_mult = getattr(config, "kv_shared_group_size", 1)
+        if self.num_kv_heads * kv_mult < tp or (self.num_kv_heads * kv_mult) % tp:
+            kv_mult = max(kv_mult, tp // math.gcd(tp, self.num_kv_heads))
+        self.kv_mult = kv_mult
+        self.num_heads_local = divide(self.num_heads, tp)
+        self.num_kv_heads_local = divide(self.num_kv_heads * kv_mult, tp)
+        sp = getattr(config, "sequence_parallel_enabled", False)
+        init = partial(_init_normal, config.initializer_range)
+        self.qkv_proj = GQAQKVColumnParallelLinear(
+            self.hidden_size, [self.num_heads * self.head_dim, self.num_kv_heads * self.head_dim],
+            bias=getattr(config, "attention_bias", False), gather_output=False, init_method=init,
+            sequence_parallel_enabled=sp, kv_size_multiplier=kv_mult, fuse_qkv=True, dtype=dtype, device=device)
+        self.o_proj = RowParallelLinear(self.num_heads * self.head_dim, self.hidden_size,
+                                        bias=getattr(config, "attention_bias", False), input_is_parallel=True,
+                                        init_method=init, sequence_parallel_enabled=sp, dtype=dtype, device=device)
+        self.rope_cache = rope_cache
+
+    def forward(self, x):
+        qkv = self.qkv_proj.forward_fused(x)  # [S, B, (nq + 2 nkv) D]
+        cos_t, sin_t = self.rope_cache.tables(qkv.device)
+        o = ops.rope_attention(qkv, cos_t, sin_t, self.num_heads_local, self.num_kv_heads_local, self.head_dim,
+                               causal=True)
+        return self.o_proj(o)
+
+
+class RopeCache:
+    """fp32 cos/sin tables shared by every layer (one per device)."""
+
+    def __init__(self, config, head_dim):
+        self.inv_freq = ops.inv_freq_from_config(config, head_dim)
+        self.max_pos = int(getattr(config, "max_position_embeddings", 8192))
+        self._cache = {}
+
+    def tables(self, device):
+        key = str(device)
+        if key not in self._cache:
+            self._cache[key] = ops.rope_tables(self.inv_freq, self.max_pos, device=device)
+        return self._cache[key]
+
+
+class LlamaDecoderLayer(nn.Module):
+    def __init__(self, config, dtype, device, rope_cache):
+        super().__init__()
+        sp = getattr(config, "sequence_parallel_enabled", False)
+        self.self_attn = LlamaAttention(config, dtype, device, rope_cache)
+        self.mlp = LlamaMLP(config, dtype, device)
+        self.input_layernorm = RMSNorm(config.hidden_size, eps=config.rms_norm_eps, sequence_parallel_enabled=sp,
+                                       dtype=dtype, device=device)
+        self.post_attention_layernorm = RMSNorm(config.hidden_size, eps=config.rms_norm_eps,
+                                                sequence_parallel_enabled=sp, dtype=dtype, device=device)
+
+    def forward(self, hidden_states, residual=None):
+        """Pre-norm block on the un-added stream: returns (mlp_out, residual) where the true hidden
+        state is mlp_out + residual (the add is fused into the next norm kernel)."""
+        if residual is None:
+            normed = self.input_layernorm(hidden_states)
+            residual = hidden_states
+        else:
+            normed, residual = self.input_layernorm(hidden_states, residual)
+        attn = self.self_attn(normed)
+        normed, residual = self.post_attention_layernorm(attn, residual)
+        return self.mlp(normed), residual
+
+
+class LlamaModel(nn.Module):
+    def __init__(self, config, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.config = config
+        sp = getattr(config, "sequence_parallel_enabled", False)
+        self.sequence_parallel_enabled = sp and get_tensor_model_parallel_size() > 1
+        head_dim = getattr(config, "head_dim", None) or config.hidden_size // config.num_attention_heads
+        self.rope_cache = RopeCache(config, head_dim)
+        init = partial(_init_normal, config.initializer_range)
+        self.embed_tokens = ParallelEmbedding(config.vocab_size, config.hidden_size, init_method=init, dtype=dtype,
+                                              device=device, sequence_parallel_enabled=self.sequence_parallel_enabled)
+        self.layers = nn.ModuleList([LlamaDecoderLayer(config, dtype, device, self.rope_cache)
+                                     for _ in range(config.num_hidden_layers)])
+        self.norm = RMSNorm(config.hidden_size, eps=config.rms_norm_eps, sequence_parallel_enabled=sp, dtype=dtype,
+                            device=device)
+        self.activation_checkpoint = getattr(config, "activation_checkpoint", None)  # None | "full"
+
+    def forward(self, input_ids: torch.Tensor) -> torch.Tensor:
+        """input_ids [B, S] -> final hidden [S(/tp), B, H] (sequence-parallel shard if SP)."""
+        ids = input_ids.t().contiguous()  # [S, B]
+        hidden = self.embed_tokens(ids)
+        residual = None
+        for layer in self.layers:
+            if self.activation_checkpoint == "full" and self.training:
+                hidden, residual = checkpoint(layer, hidden, residual, use_reentrant=False)
+            else:
+                hidden, residual = layer(hidden, residual)
+        out, _ = self.norm(hidden, residual)
+        return out
+
+
+class LlamaForCausalLM(nn.Module):
+    def __init__(self, config, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.config = config
+        self.model = LlamaModel(config, dtype, device)
+        sp = self.model.sequence_parallel_enabled
+        init = partial(_init_normal, config.initializer_range)
+        self.lm_head = ColumnParallelLinear(config.hidden_size, config.vocab_size, bias=False, gather_output=False,
+                                           init_method=init, sequence_parallel_enabled=sp, dtype=dtype, device=device)
+        if getattr(config, "tie_word_embeddings", False):
+            assert self.lm_head.weight.shape == self.model.embed_tokens.weight.shape
+            self.lm_head.weight = self.model.embed_tokens.weight
+
+    def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
+                labels: Optional[torch.Tensor] = None, position_ids=None, **unused) -> CausalLMOutput:
+        hidden = self.model(input_ids)
+        logits = self.lm_head(hidden)  # [S, B, V/tp]
+        loss = None
+        if labels is not None:
+            # predict token s+1 at position s: shift labels, ignore the last position
+            lab = labels.t()  # [S, B]
+            shifted = torch.full_like(lab, -100)
+            shifted[:-1] = lab[1:]
+            if attention_mask is not None:
+                shifted[:-1] = torch.where(attention_mask.t()[1:] > 0, shifted[:-1], torch.full_like(shifted[:-1], -100))
+            per_tok = parallel_cross_entropy(logits, shifted, inplace_backward=True)
+            n = (shifted != -100).sum().clamp(min=1)
+            loss = per_tok.sum() / n
+        return CausalLMOutput(loss=loss, logits=logits)
+
+
+def llama_config(name: str = "llama3-8b", **overrides):
+    """HF `LlamaConfig` presets for the benchmark / examples (random-init architectures)."""
+    from transformers import LlamaConfig
+
+    presets = {
+        "llama3-8b": dict(hidden_size=4096, intermediate_size=14336, num_hidden_layers=32, num_attention_heads=32,
+                          num_key_value_heads=8, vocab_size=128256, rope_theta=500000.0, max_position_embeddings=8192,
+                          rms_norm_eps=1e-5),
+        "llama3.1-8b": dict(hidden_size=4096, intermediate_size=14336, num_hidden_layers=32, num_attention_heads=32,
+                            num_key_value_heads=8, vocab_size=128256, rope_theta=500000.0,
+                            max_position_embeddings=131072, rms_norm_eps=1e-5,
+                            rope_scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                          "high_freq_factor": 4.0, "original_max_position_embeddings": 8192}),
+        "llama3.2-1b": dict(hidden_size=2048, intermediate_size=8192, num_hidden_layers=16, num_attention_heads=32,
+                            num_key_value_heads=8, vocab_size=128256, rope_theta=500000.0,
+                            max_position_embeddings=131072, rms_norm_eps=1e-5, tie_word_embeddings=True,
+                            rope_scaling={"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0,
+                                          "high_freq_factor": 4.0, "original_max_position_embeddings": 8192}),
+        "llama3-70b": dict(hidden_size=8192, intermediate_size=28672, num_hidden_layers=80, num_attention_heads=64,
+                           num_key_value_heads=8, vocab_size=128256, rope_theta=500000.0, max_position_embeddings=8192,
+                           rms_norm_eps=1e-5),
+        "llama2-7b": dict(hidden_size=4096, intermediate_size=11008, num_hidden_layers=32, num_attention_heads=32,
+                          num_key_value_heads=32, vocab_size=32000, rope_theta=10000.0, max_position_embeddings=4096,
+                          rms_norm_eps=1e-5),
+        "tiny": dict(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+                     num_key_value_heads=2, vocab_size=1024, rope_theta=10000.0, max_position_embeddings=512,
+                     rms_norm_eps=1e-5),
+    }
+    kw = dict(presets[name])
+    kw.setdefault("initializer_range", 0.02)
+    kw.update(overrides)
+    cfg = LlamaConfig(**kw)
+    for k in ("sequence_parallel_enabled", "selective_checkpoint_enabled", "kv_shared_group_size",
+              "activation_checkpoint"):
+        if k in overrides:
+            setattr(cfg, k, overrides[k])
+    return cfg

@@ -16,6 +16,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from ..parallel import comm
+
 from ._ext import ext, use_native
 
 
@@ -23,7 +25,7 @@ def _combine(stats: torch.Tensor, group, world: int):
     """stats [N, 4] local -> (M, S, target_logit, sum_logits) global over the TP group."""
     if world > 1:
         gathered = torch.empty((world,) + tuple(stats.shape), dtype=stats.dtype, device=stats.device)
-        dist.all_gather_into_tensor(gathered, stats.contiguous(), group=group)
+        comm.all_gather_into_tensor(gathered, stats.contiguous(), group=group)
     else:
         gathered = stats.unsqueeze(0)
     m = gathered[..., 0]

@@ -1,0 +1,175 @@
+"""Native mixed-precision AdamW / ZeRO-1 over flat buffers.
+
+Replaces, for the AdamW family, the reference's torch_xla ZeroRedundancyOptimizer + per-parameter
+AdamW_FP32OptimParams loop (src/neuronx_distributed/optimizer/zero_redundancy_optimizer.py:29-155,
+src/neuronx_distributed/utils/adamw_fp32_optim_params.py:31-155):
+
+* bf16 model parameters, fp32 master weights and fp32 Adam moments, all flat; each DP rank owns
+  one slice of every gradient bucket (ZeRO-1) — or everything when DP = 1;
+* one step = (finish the backward-overlapped bucket reduce-scatters) -> one coalesced TP all-reduce
+  of sequence-parallel norm grads -> flat grad-norm kernel (TP-replicated params counted once,
+  partial sums all-reduced over TP / DP / PP; the clip coefficient never leaves the device) ->
+  fused AdamW kernel per bucket slice that also writes the bf16 weights -> bucket all-gathers;
+* state_dict() saves per-parameter unflattened state on DP=1, or this rank's flat shards plus
+  the shard map under ZeRO-1 (one file per DP rank, like the reference's ZeRO checkpoints).
+"""
+
+from __future__ import annotations
+
+import math
+from collections import defaultdict
+from typing import Any, Dict, Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..parallel.grad_buffer import KIND_DUP, KIND_DUP_SP, KIND_SHARDED, FlatBuffer, find_shared_params, param_kind
+from ..parallel_layers import parallel_state as ps
+
+
+class _BufferState:
+    def __init__(self, buf: FlatBuffer, group: dict):
+        self.buf = buf
+        self.group = group
+        self.ranges = buf.shard_ranges()
+        n = sum(e - s for s, e in self.ranges)
+        dev = buf.param_data.device
+        self.master = torch.empty(n, dtype=torch.float32, device=dev)
+        off = 0
+        self.local = []  # (buffer start, buffer end, local start)
+        for s, e in self.ranges:
+            self.master[off:off + e - s].copy_(buf.param_data[s:e].float())
+            self.local.append((s, e, off))
+            off += e - s
+        self.exp_avg = torch.zeros_like(self.master)
+        self.exp_avg_sq = torch.zeros_like(self.master)
+
+
+class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
+    """AdamW (decoupled weight decay) with fp32 master weights over flat buffers; optional ZeRO-1.
+
+    `params` may be an iterable of parameters or of param-group dicts (lr, betas, eps, weight_decay).
+    """
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 zero1: bool = False, dp_group=None, grad_clipping: bool = True, max_grad_norm: float = 1.0,
+                 shared_param_ids: Optional[set] = None, sp_reduce: bool = True, bias_correction: bool = True):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        if dp_group is None and ps.model_parallel_is_initialized():
+            dp_group = ps.get_data_parallel_group()
+        self.dp_group = dp_group
+        self.zero1 = zero1
+        self.grad_clipping = grad_clipping
+        self.max_grad_norm = max_grad_norm
+        self.bias_correction = bias_correction
+        self.step_count = 0
+        self.grad_norm: Optional[torch.Tensor] = None
+        self.buffers: List[_BufferState] = []
+        shared = shared_param_ids or set()
+        for gi, g in enumerate(self.param_groups):
+            by_kind = defaultdict(list)
+            for p in g["params"]:
+                if p.requires_grad:
+                    by_kind[(param_kind(p, sp_reduce), p.dtype, p.device)].append(p)
+            for (kind, _, _), plist in by_kind.items():
+                group = self.dp_group
+                if any(getattr(p, "expert_model_parallel", False) for p in plist) and ps.model_parallel_is_initialized():
+                    group = ps.get_expert_data_parallel_group()
+                buf = FlatBuffer(plist, dp_group=group, zero1=zero1, shared_ids=shared, name=f"g{gi}:{kind}")
+                buf.kind = kind
+                self.buffers.append(_BufferState(buf, g))
+
+    # ---------------------------------------------------------------- helpers
+    def set_grad_sync(self, enabled: bool) -> None:
+        for b in self.buffers:
+            b.buf.set_sync(enabled)
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        for b in self.buffers:
+            b.buf.zero_grad()
+
+    def _tp(self):
+        if ps.model_parallel_is_initialized() and ps.get_tensor_model_parallel_size() > 1:
+            return ps.get_tensor_model_parallel_group(), ps.get_tensor_model_parallel_rank()
+        return None, 0
+
+    def _sync_grads(self):
+        for b in self.buffers:
+            b.buf.finish_grad_sync(average=True)
+        tp_group, _ = self._tp()
+        if tp_group is not None:
+            sp = [b.buf.grad_data for b in self.buffers if b.buf.kind == KIND_DUP_SP]
+            if sp:
+                flat = sp[0] if len(sp) == 1 else torch.cat(sp)
+                dist.all_reduce(flat, group=tp_group)
+                if len(sp) > 1:
+                    off = 0
+                    for g in sp:
+                        g.copy_(flat[off:off + g.numel()])
+                        off += g.numel()
+
+    def _grad_norm_sq(self) -> torch.Tensor:
+        tp_group, tp_rank = self._tp()
+        dev = self.buffers[0].master.device
+        total = torch.zeros(1, dtype=torch.float32, device=dev)
+        for b in self.buffers:
+            if b.buf.kind != KIND_SHARDED and tp_rank != 0:
+                continue
+            for s, e in b.ranges:
+                ops.flat_sumsq(b.buf.grad_data[s:e], out=total, accumulate=True)
+        if tp_group is not None:
+            dist.all_reduce(total, group=tp_group)
+        if self.zero1 and self.dp_group is not None and dist.get_world_size(group=self.dp_group) > 1:
+            dist.all_reduce(total, group=self.dp_group)
+        if ps.model_parallel_is_initialized() and ps.get_pipeline_model_parallel_size() > 1:
+            dist.all_reduce(total, group=ps.get_pipeline_model_parallel_group())
+        return total
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self._sync_grads()
+        coef = None
+        if self.grad_clipping:
+            sq = self._grad_norm_sq()
+            coef = ops.clip_coefficient(sq, self.max_grad_norm, is_sumsq=True)
+            self.grad_norm = coef[1]
+        self.step_count += 1
+        for b in self.buffers:
+            g = b.group
+            beta1, beta2 = g["betas"]
+            for (s, e, lo) in b.local:
+                n = e - s
+                ops.adamw_flat_(b.master[lo:lo + n], b.buf.grad_data[s:e], b.exp_avg[lo:lo + n], b.exp_avg_sq[lo:lo + n],
+                                b.buf.param_data[s:e], g["lr"], beta1, beta2, g["eps"], g["weight_decay"], self.step_count,
+                                grad_scale=coef, bias_correction=self.bias_correction)
+        for b in self.buffers:
+            b.buf.gather_params()
+        return loss
+
+    # ---------------------------------------------------------------- checkpointing
+    def state_dict(self) -> Dict[str, Any]:
+        groups = [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]
+        bufs = []
+        for b in self.buffers:
+            bufs.append({"name": b.buf.name, "ranges": b.ranges, "master": b.master, "exp_avg": b.exp_avg,
+                         "exp_avg_sq": b.exp_avg_sq})
+        return {"flat_optimizer": True, "step": self.step_count, "param_groups": groups, "buffers": bufs,
+                "zero1": self.zero1}
+
+    def load_state_dict(self, sd: Dict[str, Any]) -> None:
+        assert sd.get("flat_optimizer"), "not a FlatMixedPrecisionAdamW state dict"
+        self.step_count = int(sd["step"])
+        for g, sg in zip(self.param_groups, sd["param_groups"]):
+            for k, v in sg.items():
+                g[k] = v
+        for b, sb in zip(self.buffers, sd["buffers"]):
+            assert b.buf.name == sb["name"] and b.master.numel() == sb["master"].numel(), "optimizer layout mismatch"
+            b.master.copy_(sb["master"])
+            b.exp_avg.copy_(sb["exp_avg"])
+            b.exp_avg_sq.copy_(sb["exp_avg_sq"])
+            for (s, e, lo) in b.local:
+                b.buf.param_data[s:e].copy_(b.master[lo:lo + e - s])
+            b.buf.gather_params()

@@ -1,0 +1,205 @@
+"""Flat parameter / gradient buffers with bucketed, backward-overlapped data-parallel reduction.
+
+The MI355X-native replacement of the reference's end-of-step gradient handling
+(bucket_allreduce_gradients: src/neuronx_distributed/parallel_layers/grads.py:243-310, and the
+torch_xla ZeroRedundancyOptimizer internals: src/neuronx_distributed/optimizer/zero_redundancy_optimizer.py):
+
+* Parameters of one kind are re-homed into ONE contiguous bf16 buffer and get an fp32 `main_grad`
+  view into ONE contiguous fp32 gradient buffer.  Linear / norm / embedding kernels accumulate
+  weight gradients straight into `main_grad` (no `.grad` tensors, no per-step zeroing of
+  thousands of tensors: one memset per buffer).
+* The gradient buffer is cut into buckets (default 128 MiB of fp32 = `NXD_DP_BUCKET_MB`) in
+  reverse registration order, i.e. the order backward produces them.  When every parameter of a
+  bucket has reported its gradient (the `_nxd_grad_ready` hook fired by the autograd functions),
+  the bucket's reduce-scatter (ZeRO-1) or all-reduce is launched asynchronously on RCCL's stream,
+  so DP communication overlaps the rest of backward.  Buckets are padded to a multiple of
+  `dp * 16` elements so each rank's slice stays 64-byte aligned for the vectorised kernels.
+* Parameters used more than once per step (tied embeddings) delay their bucket to the final
+  synchronisation so a partial gradient is never sent.
+* Buffers are keyed by (param group, kind): kind separates TP-sharded parameters from
+  TP-replicated ones (counted once in the grad norm) and, among the latter, sequence-parallel
+  ones (norm weights / row biases whose grads are summed over TP in ONE coalesced all-reduce).
+"""
+
+from __future__ import annotations
+
+import os
+from collections import defaultdict
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import comm
+
+KIND_SHARDED = "tp_sharded"
+KIND_DUP_SP = "tp_dup_sp"
+KIND_DUP = "tp_dup"
+
+
+def param_kind(p: torch.nn.Parameter, sp_reduce: bool = True) -> str:
+    if getattr(p, "tensor_model_parallel", False) or getattr(p, "expert_model_parallel", False):
+        return KIND_SHARDED
+    if sp_reduce and getattr(p, "sequence_parallel_enabled", False):
+        return KIND_DUP_SP
+    return KIND_DUP
+
+
+def _bucket_elems() -> int:
+    return int(float(os.environ.get("NXD_DP_BUCKET_MB", "128")) * 1024 * 1024 // 4)
+
+
+class _Bucket:
+    __slots__ = ("start", "end", "params", "pending", "handle", "delayed", "out")
+
+    def __init__(self, start, end, params, delayed):
+        self.start, self.end = start, end
+        self.params = list(params)
+        self.pending = set(id(p) for p in params)
+        self.handle = None
+        self.delayed = delayed
+        self.out = None
+
+
+class FlatBuffer:
+    """One flat bf16 parameter buffer + fp32 grad buffer + DP buckets for a list of parameters."""
+
+    ALIGN = 16  # elements
+
+    def __init__(self, params: Sequence[torch.nn.Parameter], dp_group=None, zero1: bool = False,
+                 grad_dtype: torch.dtype = torch.float32, shared_ids: Optional[set] = None, name: str = ""):
+        self.params = list(params)
+        self.name = name
+        self.dp_group = dp_group
+        self.dp = dist.get_world_size(group=dp_group) if (dp_group is not None and dist.is_initialized()) else 1
+        self.dp_rank = dist.get_rank(group=dp_group) if (dp_group is not None and dist.is_initialized()) else 0
+        self.zero1 = zero1 and self.dp > 1
+        shared_ids = shared_ids or set()
+        assert self.params, "empty parameter list"
+        dev = self.params[0].device
+        pdt = self.params[0].dtype
+        assert all(p.dtype == pdt and p.device == dev for p in self.params), "mixed dtype/device in one buffer"
+        # ---- layout: reverse registration order (backward order), buckets of ~cap elements
+        cap = _bucket_elems()
+        unit = self.ALIGN * self.dp
+        offsets: Dict[int, Tuple[int, int]] = {}
+        buckets_spec: List[Tuple[int, int, List[torch.nn.Parameter]]] = []
+        pos, bstart, bparams = 0, 0, []
+        for p in reversed(self.params):
+            n = p.numel()
+            offsets[id(p)] = (pos, n)
+            pos += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+            bparams.append(p)
+            if pos - bstart >= cap:
+                end = (pos + unit - 1) // unit * unit
+                buckets_spec.append((bstart, end, bparams))
+                pos, bstart, bparams = end, end, []
+        if bparams:
+            end = (pos + unit - 1) // unit * unit
+            buckets_spec.append((bstart, end, bparams))
+            pos = end
+        self.numel = pos
+        self.param_data = torch.zeros(self.numel, dtype=pdt, device=dev)
+        self.grad_data = torch.zeros(self.numel, dtype=grad_dtype, device=dev)
+        for p in self.params:
+            off, n = offsets[id(p)]
+            view = self.param_data[off:off + n].view_as(p)
+            view.copy_(p.data)
+            p.data = view
+            p.main_grad = self.grad_data[off:off + n].view(p.shape)
+            p.grad = None
+            p._nxd_grad_ready = self._on_grad_ready
+            p._nxd_buffer = self
+        self.offsets = offsets
+        self.buckets = [_Bucket(s, e, ps, any(id(q) in shared_ids for q in ps)) for (s, e, ps) in buckets_spec]
+        self._bucket_of = {id(p): b for b in self.buckets for p in b.params}
+        self.sync_enabled = True
+        self.overlap = os.environ.get("NXD_DP_OVERLAP", "1") == "1"
+        self._hooks = []
+        for p in self.params:  # generic modules that still produce .grad
+            if p.requires_grad:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._post_accumulate))
+        # ZeRO-1 shard of this rank: slice [r*len/dp, (r+1)*len/dp) of every bucket
+        self.shard_numel = sum((b.end - b.start) // self.dp for b in self.buckets) if self.zero1 else self.numel
+
+    # ---------------------------------------------------------------- grad readiness / comm
+    def _post_accumulate(self, p):
+        if p.grad is not None:
+            p.main_grad.add_(p.grad.float() if p.main_grad.dtype == torch.float32 else p.grad)
+            p.grad = None
+        self._on_grad_ready(p)
+
+    def _on_grad_ready(self, p):
+        if not (self.sync_enabled and self.overlap) or self.dp == 1:
+            return
+        b = self._bucket_of.get(id(p))
+        if b is None or b.delayed:
+            return
+        b.pending.discard(id(p))
+        if not b.pending and b.handle is None:
+            self._launch(b)
+
+    def _launch(self, b: _Bucket):
+        g = self.grad_data[b.start:b.end]
+        if self.zero1:
+            n = (b.end - b.start) // self.dp
+            b.out = self.grad_data[b.start + self.dp_rank * n: b.start + (self.dp_rank + 1) * n]
+            b.handle = comm.reduce_scatter_tensor(b.out, g, group=self.dp_group, async_op=True)
+        else:
+            b.handle = dist.all_reduce(g, group=self.dp_group, async_op=True)
+
+    def finish_grad_sync(self, average: bool = True) -> None:
+        """Launch any bucket not yet launched, wait for all, average over DP."""
+        if self.dp == 1:
+            return
+        for b in self.buckets:
+            if b.handle is None:
+                self._launch(b)
+        for b in self.buckets:
+            b.handle.wait()
+            b.handle = None
+            b.pending = set(id(p) for p in b.params)
+            if average:
+                if self.zero1:
+                    b.out.div_(self.dp)
+                else:
+                    self.grad_data[b.start:b.end].div_(self.dp)
+
+    # ---------------------------------------------------------------- ZeRO-1 views
+    def shard_ranges(self) -> List[Tuple[int, int]]:
+        """(start, end) of this rank's slice in every bucket (whole buffer when not ZeRO-1)."""
+        if not self.zero1:
+            return [(0, self.numel)]
+        out = []
+        for b in self.buckets:
+            n = (b.end - b.start) // self.dp
+            out.append((b.start + self.dp_rank * n, b.start + (self.dp_rank + 1) * n))
+        return out
+
+    def gather_params(self) -> None:
+        """ZeRO-1: all-gather every bucket's updated bf16 slices (in place)."""
+        if not self.zero1:
+            return
+        handles = []
+        for b in self.buckets:
+            n = (b.end - b.start) // self.dp
+            full = self.param_data[b.start:b.end]
+            mine = full[self.dp_rank * n:(self.dp_rank + 1) * n]
+            handles.append(comm.all_gather_into_tensor(full, mine, group=self.dp_group, async_op=True))
+        for h in handles:
+            h.wait()
+
+    def zero_grad(self) -> None:
+        self.grad_data.zero_()
+
+    def set_sync(self, enabled: bool) -> None:
+        self.sync_enabled = enabled
+
+
+def find_shared_params(model: torch.nn.Module) -> set:
+    """ids of parameters registered in more than one module (e.g. tied embeddings)."""
+    count = defaultdict(int)
+    for _, m in model.named_modules(remove_duplicate=False):
+        for _, p in m.named_parameters(recurse=False):
+            count[id(p)] += 1
+    return {k for k, v in count.items() if v > 1}

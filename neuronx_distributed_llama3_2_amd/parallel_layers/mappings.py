@@ -12,6 +12,8 @@ from __future__ import annotations
 
 import torch
 import torch.distributed as dist
+
+from ..parallel import comm
 from torch import Tensor
 
 from .parallel_state import (
@@ -72,7 +74,7 @@ def _split_along_first_dim(input_: Tensor) -> Tensor:
 def _gather_along_dim_0(x: Tensor, _dim: int, group=None) -> Tensor:
     ws = dist.get_world_size(group=group)
     out = torch.empty((ws * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    comm.all_gather_into_tensor(out, x.contiguous(), group=group)
     return out
 
 
@@ -96,7 +98,7 @@ def _reduce_scatter_dim_0(x: Tensor, _dim: int, group=None) -> Tensor:
     ws = dist.get_world_size(group=group)
     assert x.shape[0] % ws == 0, f"dim {x.shape[0]} not divisible by TP size {ws}"
     out = torch.empty((x.shape[0] // ws,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.reduce_scatter_tensor(out, x.contiguous(), group=group)
+    comm.reduce_scatter_tensor(out, x.contiguous(), group=group)
     return out
 
 
@@ -125,7 +127,7 @@ def _all_to_all_in_expert_parallel_region(x: Tensor, split_dim: int, concat_dim:
     concat_dim %= x.dim()
     xs = x.movedim(split_dim, 0).contiguous()
     out = torch.empty_like(xs)
-    dist.all_to_all_single(out, xs, group=group)
+    comm.all_to_all_single(out, xs, group=group)
     chunks = out.chunk(ws, dim=0)
     chunks = [c.movedim(0, split_dim) for c in chunks]
     return torch.cat(chunks, dim=concat_dim).contiguous()
