@@ -112,7 +112,8 @@ void flash_attn_bwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == (int64_t)B * Hq * Sq, "bad lse");
   auto opts = q.options().dtype(at::kFloat);
   at::Tensor delta = at::empty({(int64_t)B * Hq * Sq}, opts);
-  at::Tensor dq_acc = at::empty({(int64_t)B * Hq * Sq * D}, opts);
+  const int64_t Sq_pad = (Sq + 31) / 32 * 32;  // bwd kernel pads query rows to its 32-row tile
+  at::Tensor dq_acc = at::empty({(int64_t)B * Hq * Sq_pad * D}, opts);
   check_rc(nxd::flash_attn_bwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                                       lse.data_ptr<float>(), delta.data_ptr<float>(), dq_acc.data_ptr<float>(), dq.data_ptr(),
                                       dk.data_ptr(), dv.data_ptr(), qs, ks, vs, os, dos, dqs, dks, dvs, B, Sq, Sk, Hq, Hkv, D,

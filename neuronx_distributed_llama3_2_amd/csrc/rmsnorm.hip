@@ -125,14 +125,24 @@ __global__ void __launch_bounds__(256) bwd_kernel(const uint16_t* __restrict__ d
   }
 }
 
-// dw[c] = sum_g part[g][c]  (fp32 out; optionally accumulated into an fp32 main_grad)
+// dw[c] = sum_g part[g][c]  (fp32 out; optionally accumulated into an fp32 main_grad).
+// 32 columns x 8 row-groups per workgroup (H/32 workgroups), LDS reduction of the 8 partials.
 __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, float* __restrict__ out, int G, int H,
                                                     int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= H) return;
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
   float s = 0.f;
-  for (int gi = 0; gi < G; ++gi) s += part[(int64_t)gi * H + c];
-  out[c] = accumulate ? out[c] + s : s;
+  if (c < H)
+    for (int gi = rg; gi < G; gi += 8) s += part[(int64_t)gi * H + c];
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && c < H) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][cl];
+    out[c] = accumulate ? out[c] + t : t;
+  }
 }
 
 }  // namespace rms
@@ -177,7 +187,7 @@ int rmsnorm_bwd_launch(const void* dy, const void* h, const void* w, const float
   else if (vpt <= 8) RMS_BWD(8);
   else return -2;
 #undef RMS_BWD
-  hipLaunchKernelGGL(colsum_kernel, dim3((H + 255) / 256), dim3(256), 0, stream, dw_part, dw, G, H, accumulate_dw);
+  hipLaunchKernelGGL(colsum_kernel, dim3((H + 31) / 32), dim3(256), 0, stream, dw_part, dw, G, H, accumulate_dw);
   return (int)hipGetLastError();
 }
 
