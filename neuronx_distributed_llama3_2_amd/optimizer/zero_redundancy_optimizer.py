@@ -1,0 +1,154 @@
+"""ZeRO-1 optimizers with the reference's class names and constructor
+(src/neuronx_distributed/optimizer/zero_redundancy_optimizer.py:29-362).
+
+`NeuronZero1Optimizer(params, optimizer_class, grad_clipping=True, max_norm=..., sharding_groups=...,
+grad_norm_groups=..., pin_layout=..., coalesce_cc=..., use_grad_acc_hook=..., higher_cc_precision=...,
+save_master_weights=..., **defaults)`:
+
+* AdamW family (torch.optim.AdamW / Adam, AdamW_FP32OptimParams): the native flat path
+  (FlatMixedPrecisionAdamW, zero1=True) — bucketed backward-overlapped reduce-scatter, fused
+  AdamW kernel on this rank's fp32 shard, bucket all-gather of the bf16 weights.
+* Any other optimizer class: generic ZeRO-1 on the same flat buffers — this rank's fp32 master
+  shard of every bucket becomes one parameter of an `optimizer_class` instance whose `.grad` is the
+  reduce-scattered fp32 gradient slice (elementwise optimizers are exact; per-tensor statistics
+  such as LAMB trust ratios are computed per bucket slice).
+* Expert-parallel parameters (`expert_model_parallel`) are sharded over the expert-data-parallel
+  group (NeuronEPZero1Optimizer semantics) automatically.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..parallel.grad_buffer import KIND_DUP_SP, KIND_SHARDED, FlatBuffer, param_kind
+from ..parallel_layers import parallel_state as ps
+from .flat_optimizer import FlatMixedPrecisionAdamW
+
+_ADAM_NAMES = {"AdamW", "Adam", "AdamW_FP32OptimParams", "FusedAdam"}
+
+
+def _is_adam_family(cls) -> bool:
+    return getattr(cls, "__name__", "") in _ADAM_NAMES
+
+
+class _GenericZero1(torch.optim.Optimizer):
+    def __init__(self, params, optimizer_class, dp_group=None, grad_clipping=True, max_norm=1.0, **defaults):
+        super().__init__(params, dict(defaults))
+        self.dp_group = dp_group if dp_group is not None else (
+            ps.get_data_parallel_group() if ps.model_parallel_is_initialized() else None)
+        self.grad_clipping, self.max_norm = grad_clipping, max_norm
+        self.buffers = []
+        inner_groups = []
+        for g in self.param_groups:
+            plist = [p for p in g["params"] if p.requires_grad]
+            if not plist:
+                continue
+            kinds = {}
+            for p in plist:
+                kinds.setdefault(param_kind(p), []).append(p)
+            for kind, ps_ in kinds.items():
+                buf = FlatBuffer(ps_, dp_group=self.dp_group, zero1=True, name=kind)
+                buf.kind = kind
+                masters = []
+                for s, e in buf.shard_ranges():
+                    m = torch.nn.Parameter(buf.param_data[s:e].detach().float().clone())
+                    m._range = (s, e)
+                    masters.append(m)
+                self.buffers.append((buf, masters))
+                gi = {k: v for k, v in g.items() if k != "params"}
+                gi["params"] = masters
+                inner_groups.append(gi)
+        self.inner = optimizer_class(inner_groups, **defaults)
+        self.grad_norm = None
+
+    def set_grad_sync(self, enabled: bool) -> None:
+        for b, _ in self.buffers:
+            b.set_sync(enabled)
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        for b, _ in self.buffers:
+            b.zero_grad()
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        for b, _ in self.buffers:
+            b.finish_grad_sync()
+        tp = ps.get_tensor_model_parallel_size() if ps.model_parallel_is_initialized() else 1
+        if tp > 1:
+            for b, _ in self.buffers:
+                if b.kind == KIND_DUP_SP:
+                    dist.all_reduce(b.grad_data, group=ps.get_tensor_model_parallel_group())
+        for b, masters in self.buffers:
+            for m in masters:
+                s, e = m._range
+                m.grad = b.grad_data[s:e]
+        if self.grad_clipping:
+            dev = self.buffers[0][0].grad_data.device
+            sq = torch.zeros(1, dtype=torch.float32, device=dev)
+            tp_rank = ps.get_tensor_model_parallel_rank() if ps.model_parallel_is_initialized() else 0
+            for b, masters in self.buffers:
+                if b.kind != KIND_SHARDED and tp_rank != 0:
+                    continue
+                for m in masters:
+                    ops.flat_sumsq(m.grad, out=sq, accumulate=True)
+            if tp > 1:
+                dist.all_reduce(sq, group=ps.get_tensor_model_parallel_group())
+            if self.dp_group is not None and dist.get_world_size(group=self.dp_group) > 1:
+                dist.all_reduce(sq, group=self.dp_group)
+            coef = ops.clip_coefficient(sq, self.max_norm)
+            self.grad_norm = coef[1]
+            for b, masters in self.buffers:
+                for m in masters:
+                    m.grad.mul_(coef[0])
+        loss = self.inner.step(closure)
+        for b, masters in self.buffers:
+            for m in masters:
+                s, e = m._range
+                b.param_data[s:e].copy_(m.detach())
+            b.gather_params()
+        return loss
+
+    def state_dict(self) -> Dict[str, Any]:
+        return {"generic_zero1": True, "inner": self.inner.state_dict(),
+                "masters": [[m.detach() for m in ms] for _, ms in self.buffers]}
+
+    def load_state_dict(self, sd: Dict[str, Any]) -> None:
+        self.inner.load_state_dict(sd["inner"])
+        for (b, ms), saved in zip(self.buffers, sd["masters"]):
+            for m, t in zip(ms, saved):
+                m.data.copy_(t)
+                s, e = m._range
+                b.param_data[s:e].copy_(m.detach())
+            b.gather_params()
+
+
+def NeuronZero1Optimizer(params, optimizer_class=torch.optim.AdamW, grad_clipping: bool = True, max_norm: float = 1.0,
+                         sharding_groups=None, grad_norm_groups=None, pin_layout: bool = False, coalesce_cc: bool = True,
+                         use_grad_acc_hook: bool = True, higher_cc_precision: bool = True,
+                         save_master_weights: bool = False, lazy_init: bool = False, optimizer_dtype=None,
+                         shared_param_ids: Optional[set] = None, **defaults):
+    """Factory with the reference signature; returns the MI355X-native implementation."""
+    dp_group = None
+    if isinstance(sharding_groups, (torch.distributed.ProcessGroup,)):
+        dp_group = sharding_groups
+    elif ps.model_parallel_is_initialized():
+        dp_group = ps.get_data_parallel_group()
+    if _is_adam_family(optimizer_class):
+        kw = {k: v for k, v in defaults.items() if k in ("lr", "betas", "eps", "weight_decay")}
+        opt = FlatMixedPrecisionAdamW(params, zero1=True, dp_group=dp_group, grad_clipping=grad_clipping,
+                                      max_grad_norm=max_norm, shared_param_ids=shared_param_ids, **kw)
+    else:
+        opt = _GenericZero1(params, optimizer_class, dp_group=dp_group, grad_clipping=grad_clipping, max_norm=max_norm,
+                            **defaults)
+    opt.save_master_weights = save_master_weights
+    return opt
+
+
+def NeuronEPZero1Optimizer(params, optimizer_class=torch.optim.AdamW, **kwargs):
+    """Expert-parallel ZeRO-1: expert params are sharded over the expert-data-parallel group and
+    dense params over the full DP group (handled per buffer by the flat optimizer)."""
+    return NeuronZero1Optimizer(params, optimizer_class, **kwargs)
