@@ -38,13 +38,19 @@ from ...parallel_layers.parallel_state import get_tensor_model_parallel_size
 from ...parallel_layers.utils import divide
 
 
-@dataclass
-class CausalLMOutput:
-    loss: Optional[torch.Tensor] = None
-    logits: Optional[torch.Tensor] = None
+class CausalLMOutput(dict):
+    """{loss, logits} with attribute access (a dict, so torch.fx can return it from a traced graph)."""
 
-    def __getitem__(self, i):
-        return (self.loss, self.logits)[i] if self.loss is not None else (self.logits,)[i]
+    def __init__(self, loss=None, logits=None):
+        super().__init__(loss=loss, logits=logits)
+
+    @property
+    def loss(self):
+        return self["loss"]
+
+    @property
+    def logits(self):
+        return self["logits"]
 
 
 def _init_normal(std, w):
@@ -169,12 +175,14 @@ class LlamaModel(nn.Module):
         hidden = self.embed_tokens(ids)
         residual = None
         for layer in self.layers:
+            # index (not unpack) the (hidden, residual) pair: keeps the loop torch.fx-traceable for
+            # pipeline partitioning, where each decoder layer is a leaf
             if self.activation_checkpoint == "full" and self.training:
-                hidden, residual = checkpoint(layer, hidden, residual, use_reentrant=False)
+                res = checkpoint(layer, hidden, residual, use_reentrant=False)
             else:
-                hidden, residual = layer(hidden, residual)
-        out, _ = self.norm(hidden, residual)
-        return out
+                res = layer(hidden, residual)
+            hidden, residual = res[0], res[1]
+        return self.norm(hidden, residual)[0]
 
 
 class LlamaForCausalLM(nn.Module):
@@ -198,10 +206,10 @@ class LlamaForCausalLM(nn.Module):
         if labels is not None:
             # predict token s+1 at position s: shift labels, ignore the last position
             lab = labels.t()  # [S, B]
-            shifted = torch.full_like(lab, -100)
-            shifted[:-1] = lab[1:]
+            nxt = lab[1:]
             if attention_mask is not None:
-                shifted[:-1] = torch.where(attention_mask.t()[1:] > 0, shifted[:-1], torch.full_like(shifted[:-1], -100))
+                nxt = torch.where(attention_mask.t()[1:] > 0, nxt, torch.full_like(nxt, -100))
+            shifted = torch.cat([nxt, torch.full_like(lab[:1], -100)], dim=0)
             per_tok = parallel_cross_entropy(logits, shifted, inplace_backward=True)
             n = (shifted != -100).sum().clamp(min=1)
             loss = per_tok.sum() / n

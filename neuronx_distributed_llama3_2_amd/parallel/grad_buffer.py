@@ -111,9 +111,16 @@ class FlatBuffer:
             p._nxd_grad_ready = self._on_grad_ready
             p._nxd_buffer = self
         self.offsets = offsets
-        self.buckets = [_Bucket(s, e, ps, any(id(q) in shared_ids for q in ps)) for (s, e, ps) in buckets_spec]
+        # pipeline-shared parameters (tied across stages) are summed across stages at the end of the
+        # step, so their bucket must wait for the final synchronisation too
+        self.buckets = [_Bucket(s, e, ps, any(id(q) in shared_ids or getattr(q, "_nxd_pp_shared", False) for q in ps))
+                        for (s, e, ps) in buckets_spec]
         self._bucket_of = {id(p): b for b in self.buckets for p in b.params}
-        self.sync_enabled = True
+        # Overlap is ARMED per step: the training loop (or the pipeline runtime) calls set_sync(True)
+        # right before the backward of the LAST micro-batch; finish_grad_sync() disarms it.  Unarmed,
+        # every bucket is reduced at the optimizer step (always correct under grad accumulation).
+        self.sync_enabled = False
+        _LIVE_BUFFERS.append(self)
         self.overlap = os.environ.get("NXD_DP_OVERLAP", "1") == "1"
         self._hooks = []
         for p in self.params:  # generic modules that still produce .grad
@@ -150,6 +157,7 @@ class FlatBuffer:
 
     def finish_grad_sync(self, average: bool = True) -> None:
         """Launch any bucket not yet launched, wait for all, average over DP."""
+        self.sync_enabled = False
         if self.dp == 1:
             return
         for b in self.buckets:
@@ -194,6 +202,28 @@ class FlatBuffer:
 
     def set_sync(self, enabled: bool) -> None:
         self.sync_enabled = enabled
+
+
+class _LiveSet:
+    def __init__(self):
+        import weakref
+
+        self._s = weakref.WeakSet()
+
+    def append(self, b):
+        self._s.add(b)
+
+    def __iter__(self):
+        return iter(list(self._s))
+
+
+_LIVE_BUFFERS = _LiveSet()
+
+
+def arm_grad_sync(enabled: bool = True) -> None:
+    """Arm (or disarm) backward-overlapped DP reduction on every live flat buffer."""
+    for b in list(_LIVE_BUFFERS):
+        b.set_sync(enabled)
 
 
 def find_shared_params(model: torch.nn.Module) -> set:

@@ -78,3 +78,55 @@ def test_plain_optimizer_path():
     run_distributed(_train, 2, 2, False, 3, os.path.join(d, "p.pt"))
     p = torch.load(os.path.join(d, "p.pt"))
     assert p[-1] < p[0]
+
+
+def _train_pp(rank, world, pp, steps, out):
+    import neuronx_distributed_llama3_2_amd as nxd
+    from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import (
+        LlamaDecoderLayer,
+        LlamaForCausalLM,
+        llama_config,
+    )
+
+    pcfg = {"transformer_layer_cls": LlamaDecoderLayer, "num_microbatches": 2, "input_names": ["input_ids", "labels"],
+            "auto_partition": True, "broadcast_and_average_loss": True}
+    cfg_nxd = nxd.neuronx_distributed_config(pipeline_parallel_size=pp, pipeline_config=pcfg,
+                                            optimizer_config={"zero_one_enabled": True, "grad_clipping": True,
+                                                              "max_grad_norm": 1.0})
+    cfg = llama_config("tiny", num_hidden_layers=4)
+    torch.manual_seed(0)
+    model = nxd.initialize_parallel_model(cfg_nxd, LlamaForCausalLM, cfg, torch.float32)
+    opt = nxd.initialize_parallel_optimizer(cfg_nxd, torch.optim.AdamW, model.parameters(), lr=3e-3,
+                                            betas=(0.9, 0.95), weight_decay=0.0)
+    dp, dpr = ps.get_data_parallel_size(), ps.get_data_parallel_rank()
+    g = torch.Generator().manual_seed(7)
+    batches = [torch.randint(0, cfg.vocab_size, (8, 16), generator=g) for _ in range(2)]
+    losses = []
+    for step in range(steps):
+        local = batches[step % 2].chunk(dp)[dpr]
+        if pp > 1:
+            loss = model.run_train(input_ids=local, labels=local)
+        else:
+            # same micro-batching as the pipeline: mean of two half-batch losses
+            loss = 0
+            for mb in local.chunk(2):
+                l = model(mb, labels=mb).loss / 2
+                l.backward()
+                loss = loss + l.detach()
+        opt.step()
+        opt.zero_grad()
+        l = torch.as_tensor(loss, dtype=torch.float32).clone().reshape(1)
+        dist.all_reduce(l)
+        losses.append(float(l) / world)
+    if rank == 0:
+        torch.save(losses, out)
+
+
+def test_pp2_dp2_zero1_matches_dp2():
+    d = tempfile.mkdtemp()
+    run_distributed(_train_pp, 2, 1, 4, os.path.join(d, "ref.pt"))
+    run_distributed(_train_pp, 4, 2, 4, os.path.join(d, "pp.pt"))
+    a, b = torch.load(os.path.join(d, "ref.pt")), torch.load(os.path.join(d, "pp.pt"))
+    assert a[-1] < a[0]
+    for x, y in zip(a, b):
+        assert abs(x - y) < 1e-4, (a, b)
