@@ -1,0 +1,131 @@
+"""Llama-3 / 3.1 / 3.2 inference model: tensor-parallel, persistent KV cache, fused CDNA4 kernels
+(reference: examples/inference/llama3/neuron_modeling_llama.py:117-446 and the device graph of
+examples/inference/modules/model_base.py:334-451).
+
+The module IS the training `LlamaForCausalLM` (same parameter names, so training checkpoints and
+converted HF weights load directly) with an inference forward:
+
+* context encoding (prefill, T tokens per sequence): fused residual+RMSNorm kernel -> one fused
+  QKV GEMM -> in-place RoPE on the q/k columns of that buffer (one launch for both) -> in-place
+  KV-cache write -> causal flash attention (flash_attn_fwd.hip) on strided views -> o_proj
+  (+ TP all-reduce) -> add+norm -> gate_up GEMM -> SwiGLU kernel -> down (+ all-reduce); only the
+  last valid position of every sequence goes through the final norm and the lm_head;
+* token generation (T = 1, or T = speculation length): same block with the flash-decoding
+  kernel (inference.hip) reading the KV cache up to a per-sequence DEVICE length, so a decode
+  step has static shapes and no host sync — it is captured into hipGraphs (inference/graphs.py).
+
+KV cache: ONE allocation [layers, 2, max_batch, kv_heads_local, max_len, head_dim] (bf16);
+`seq_ids` selects cache rows (continuous batching).
+"""
+
+from __future__ import annotations
+
+import copy
+import math
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from .. import ops
+from ..models.llama.modeling_llama import LlamaForCausalLM
+from ..parallel_layers import parallel_state as ps
+from ..parallel_layers.parallel_state import get_tensor_model_parallel_size
+
+
+class LlamaInferenceModel(LlamaForCausalLM):
+    def __init__(self, config, dtype=torch.bfloat16, device=None):
+        cfg = copy.copy(config)
+        cfg.sequence_parallel_enabled = False
+        super().__init__(cfg, dtype=dtype, device=device)
+        attn0 = self.model.layers[0].self_attn
+        self.nq, self.nkv, self.head_dim = attn0.num_heads_local, attn0.num_kv_heads_local, attn0.head_dim
+        self.tp = get_tensor_model_parallel_size()
+        self.kv_cache: Optional[torch.Tensor] = None
+        self.eps = float(config.rms_norm_eps)
+        self.eval()
+        for p in self.parameters():
+            p.requires_grad_(False)
+
+    # ------------------------------------------------------------------ KV cache
+    def setup_kv_cache(self, max_batch: int, max_len: int, device=None) -> torch.Tensor:
+        device = device or self.lm_head.weight.device
+        L = len(self.model.layers)
+        shape = (L, 2, max_batch, self.nkv, max_len, self.head_dim)
+        if self.kv_cache is None or tuple(self.kv_cache.shape) != shape or self.kv_cache.device != torch.device(device):
+            self.kv_cache = torch.zeros(shape, dtype=self.lm_head.weight.dtype, device=device)
+        return self.kv_cache
+
+    def reset_kv_cache(self) -> None:
+        if self.kv_cache is not None:
+            self.kv_cache.zero_()
+
+    # ------------------------------------------------------------------ collectives
+    def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.tp > 1:
+            dist.all_reduce(x, group=ps.get_tensor_model_parallel_group())
+        return x
+
+    def _gather_vocab(self, logits: torch.Tensor) -> torch.Tensor:
+        if self.tp == 1:
+            return logits
+        from ..parallel import comm
+
+        out = torch.empty((self.tp,) + tuple(logits.shape), dtype=logits.dtype, device=logits.device)
+        comm.all_gather_into_tensor(out, logits.contiguous(), group=ps.get_tensor_model_parallel_group())
+        return torch.movedim(out, 0, -2).reshape(logits.shape[:-1] + (self.tp * logits.shape[-1],))
+
+    # ------------------------------------------------------------------ forward
+    @torch.no_grad()
+    def forward_tokens(self, input_ids: torch.Tensor, positions: torch.Tensor, seq_ids: Optional[torch.Tensor] = None,
+                       cache_len: Optional[torch.Tensor] = None, last_index: Optional[torch.Tensor] = None,
+                       prefill: bool = False) -> torch.Tensor:
+        """input_ids [B, T]; positions [B, T] (int64) absolute positions of the new tokens;
+        seq_ids [B] cache rows; cache_len [B] int32 valid cache length AFTER this step (decode);
+        last_index [B] -> logits [B, V] of that token per sequence, else logits [B, T, V].
+        prefill=True: the new tokens start at position 0 (causal flash attention over them)."""
+        assert self.kv_cache is not None, "call setup_kv_cache() first"
+        B, T = input_ids.shape
+        nq, nkv, D = self.nq, self.nkv, self.head_dim
+        W = (nq + 2 * nkv) * D
+        cos_t, sin_t = self.model.rope_cache.tables(input_ids.device)
+        pos_flat = positions.reshape(-1)
+        pos0 = positions[:, 0].to(torch.int32)
+        emb = self.model.embed_tokens
+        x = ops.vocab_parallel_embedding(input_ids, emb.weight, emb.start_index)
+        x = self._all_reduce(x)
+        residual = None
+        for i, layer in enumerate(self.model.layers):
+            attn, mlp = layer.self_attn, layer.mlp
+            h, residual = self._norm(x, layer.input_layernorm.weight, residual)
+            w_qkv, b_qkv = attn.qkv_proj._fused_weight_bias()
+            qkv = F.linear(h, w_qkv, b_qkv)  # [B, T, W]
+            ops.rope_inplace_(qkv.view(B * T, W), 0, nq + nkv, D, cos_t, sin_t, pos_flat)
+            q = qkv.view(B, T, nq + 2 * nkv, D)[:, :, :nq]
+            k = qkv.view(B, T, nq + 2 * nkv, D)[:, :, nq:nq + nkv]
+            v = qkv.view(B, T, nq + 2 * nkv, D)[:, :, nq + nkv:]
+            kc, vc = self.kv_cache[i, 0], self.kv_cache[i, 1]
+            ops.kv_cache_write(k, v, kc, vc, pos0, seq_ids)
+            if prefill:
+                o, _ = ops.flash_attn_fwd_lse(q, k, v, causal=True)
+            else:
+                o = ops.decode_attention(q, kc, vc, cache_len, seq_ids)
+            x = F.linear(o.reshape(B, T, nq * D), attn.o_proj.weight, attn.o_proj.bias)
+            x = self._all_reduce(x)
+            h, residual = self._norm(x, layer.post_attention_layernorm.weight, residual)
+            a = ops.swiglu(F.linear(h, mlp.gate_up_proj.weight))
+            x = self._all_reduce(F.linear(a, mlp.down_proj.weight))
+        if last_index is not None:
+            rows = torch.arange(B, device=x.device)
+            x = x[rows, last_index]
+            residual = residual[rows, last_index]
+        h, _ = self._norm(x, self.model.norm.weight, residual)
+        logits = F.linear(h, self.lm_head.weight)
+        return self._gather_vocab(logits)
+
+    def _norm(self, x, w, residual):
+        if residual is None:
+            y, _ = ops.rms_norm(x, w, self.eps)
+            return y, x
+        return ops.rms_norm(x, w, self.eps, residual)

@@ -199,6 +199,8 @@ class GQAQKVColumnParallelLinear(BaseParallelLinear):
             set_tensor_model_parallel_attributes(self.weight_qkv, True, 0, 1)
             setattr(self.weight_qkv, "fused_qkv", True)
             setattr(self.weight_qkv, "num_partitions", get_tensor_model_parallel_size())
+            # full-row layout needed to (un)shard checkpoints: (q rows, kv rows, kv replication)
+            setattr(self.weight_qkv, "qkv_split", (self.output_sizes[0], self.output_sizes[1], self.kv_size_multiplier))
         else:
             self.weight_q = Parameter(shards[0])
             self.weight_k = Parameter(shards[1])
@@ -209,6 +211,7 @@ class GQAQKVColumnParallelLinear(BaseParallelLinear):
             if self.fuse_qkv:
                 self.bias_qkv = Parameter(torch.zeros(q_l + 2 * kv_l, dtype=self.dtype, device=self.device))
                 set_tensor_model_parallel_attributes(self.bias_qkv, True, 0, 1)
+                setattr(self.bias_qkv, "qkv_split", (self.output_sizes[0], self.output_sizes[1], self.kv_size_multiplier))
             else:
                 self.bias_q = Parameter(torch.zeros(q_l, dtype=self.dtype, device=self.device))
                 self.bias_k = Parameter(torch.zeros(kv_l, dtype=self.dtype, device=self.device))

@@ -32,8 +32,14 @@ def llama3_inv_freq(dim: int, base: float = 500000.0, factor: Optional[float] = 
 
 
 def inv_freq_from_config(config, head_dim: int) -> torch.Tensor:
-    base = float(getattr(config, "rope_theta", 10000.0))
-    rs = getattr(config, "rope_scaling", None) or {}
+    # transformers >= 5 keeps theta and scaling in `rope_parameters`; older configs use
+    # `rope_theta` + `rope_scaling`
+    rp = getattr(config, "rope_parameters", None) or {}
+    rs = rp if isinstance(rp, dict) and rp else (getattr(config, "rope_scaling", None) or {})
+    base = rs.get("rope_theta") if isinstance(rs, dict) else None
+    if base is None:
+        base = getattr(config, "rope_theta", None)
+    base = float(base if base is not None else 10000.0)
     rtype = rs.get("rope_type", rs.get("type")) if isinstance(rs, dict) else None
     if rtype == "llama3":
         return llama3_inv_freq(head_dim, base, float(rs["factor"]), float(rs.get("low_freq_factor", 1.0)),

@@ -19,7 +19,7 @@ import torch.distributed as dist
 from torch import nn
 
 _PARALLEL_ATTRS = ("tensor_model_parallel", "partition_dim", "partition_stride", "num_partitions",
-                   "sequence_parallel_enabled", "expert_model_parallel", "shared", "fused_qkv")
+                   "sequence_parallel_enabled", "expert_model_parallel", "shared", "fused_qkv", "qkv_split")
 
 
 def analyze_shared_parameters(module: nn.Module, prefix: str = "") -> List[List[str]]:
