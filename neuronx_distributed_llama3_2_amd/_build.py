@@ -1,7 +1,8 @@
 """In-tree build of the CDNA4 extension `_C` (hipcc --offload-arch=gfx950, no hipify, no JIT cache).
 
 Every `csrc/*.hip` file is a self-contained kernel translation unit (HIP runtime headers only, so
-each compiles in seconds); `csrc/bindings.cpp` is the single TU that includes the torch headers.
+each compiles in seconds); the `csrc/*.cpp` host TUs (pybind bindings, the hipBLASLt GEMM tuner)
+are the only ones that include the torch headers.
 Objects are cached under `build/` keyed on source + header mtimes and compiled in parallel, then
 linked into `neuronx_distributed_llama3_2_amd/_C*.so` next to this file, so the built library
 travels with the source tree (e.g. to a GPU box) and is what `import` loads.
@@ -51,7 +52,7 @@ def _torch_flags():
     ]
     libdir = tdir / "lib"
     libs = [f"-L{libdir}", f"-Wl,-rpath,{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip",
-            "-ltorch_hip", "-lamdhip64"]
+            "-ltorch_hip", "-lamdhip64", "-lhipblaslt"]
     return inc, defs, libs
 
 
@@ -84,11 +85,12 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         objs.append(obj)
         if force or _needs_build(src, obj, headers):
             jobs_list.append([hipcc, *common, "-c", str(src), "-o", str(obj)])
-    bind = CSRC / "bindings.cpp"
-    bobj = BUILD_DIR / "bindings.o"
-    objs.append(bobj)
-    if force or _needs_build(bind, bobj, headers):
-        jobs_list.append([hipcc, "-x", "hip", *common, *inc, *defs, "-c", str(bind), "-o", str(bobj)])
+    # host-side C++ translation units that include the torch headers (bindings, hipBLASLt tuner)
+    for src in sorted(CSRC.glob("*.cpp")):
+        obj = BUILD_DIR / (src.stem + ".o")
+        objs.append(obj)
+        if force or _needs_build(src, obj, headers):
+            jobs_list.append([hipcc, "-x", "hip", *common, *inc, *defs, "-c", str(src), "-o", str(obj)])
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
     failures = []
     if jobs_list:

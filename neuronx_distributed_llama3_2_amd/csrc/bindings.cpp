@@ -443,7 +443,10 @@ void topk_sample(at::Tensor x, int64_t k, double temperature, c10::optional<at::
 
 }  // namespace
 
+void register_gemm(pybind11::module& m);  // gemm.cpp
+
 PYBIND11_MODULE(_C, m) {
+  register_gemm(m);
   m.doc() = "CDNA4 (gfx950) kernels of neuronx_distributed_llama3_2_amd";
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);

@@ -29,6 +29,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops.gemm import linear as _linear
 from ..models.llama.modeling_llama import LlamaForCausalLM
 from ..parallel_layers import parallel_state as ps
 from ..parallel_layers.parallel_state import get_tensor_model_parallel_size
@@ -100,7 +101,7 @@ class LlamaInferenceModel(LlamaForCausalLM):
             attn, mlp = layer.self_attn, layer.mlp
             h, residual = self._norm(x, layer.input_layernorm.weight, residual)
             w_qkv, b_qkv = attn.qkv_proj._fused_weight_bias()
-            qkv = F.linear(h, w_qkv, b_qkv)  # [B, T, W]
+            qkv = _linear(h, w_qkv, b_qkv)  # [B, T, W]
             ops.rope_inplace_(qkv.view(B * T, W), 0, nq + nkv, D, cos_t, sin_t, pos_flat)
             q = qkv.view(B, T, nq + 2 * nkv, D)[:, :, :nq]
             k = qkv.view(B, T, nq + 2 * nkv, D)[:, :, nq:nq + nkv]
@@ -111,17 +112,17 @@ class LlamaInferenceModel(LlamaForCausalLM):
                 o, _ = ops.flash_attn_fwd_lse(q, k, v, causal=True)
             else:
                 o = ops.decode_attention(q, kc, vc, cache_len, seq_ids)
-            x = F.linear(o.reshape(B, T, nq * D), attn.o_proj.weight, attn.o_proj.bias)
+            x = _linear(o.reshape(B, T, nq * D), attn.o_proj.weight, attn.o_proj.bias)
             x = self._all_reduce(x)
             h, residual = self._norm(x, layer.post_attention_layernorm.weight, residual)
-            a = ops.swiglu(F.linear(h, mlp.gate_up_proj.weight))
-            x = self._all_reduce(F.linear(a, mlp.down_proj.weight))
+            a = ops.swiglu(_linear(h, mlp.gate_up_proj.weight))
+            x = self._all_reduce(_linear(a, mlp.down_proj.weight))
         if last_index is not None:
             rows = torch.arange(B, device=x.device)
             x = x[rows, last_index]
             residual = residual[rows, last_index]
         h, _ = self._norm(x, self.model.norm.weight, residual)
-        logits = F.linear(h, self.lm_head.weight)
+        logits = _linear(h, self.lm_head.weight)
         return self._gather_vocab(logits)
 
     def _norm(self, x, w, residual):

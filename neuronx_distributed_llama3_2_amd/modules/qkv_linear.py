@@ -22,6 +22,7 @@ import torch
 import torch.distributed as dist
 
 from ..parallel import comm
+from ..ops import gemm as _gemm
 from torch import nn
 from torch.nn.parameter import Parameter
 
@@ -33,7 +34,8 @@ from ..parallel_layers.layers import (
     _initialize_parameter,
     _device_of,
 )
-from ..parallel_layers.mappings import _gather_along_first_dim, copy_to_tensor_model_parallel_region, gather_from_tensor_model_parallel_region
+from ..parallel_layers import sp
+from ..parallel_layers.mappings import copy_to_tensor_model_parallel_region, gather_from_tensor_model_parallel_region
 from ..parallel_layers.parallel_state import (
     get_tensor_model_parallel_group,
     get_tensor_model_parallel_rank,
@@ -91,10 +93,13 @@ class GQAQKVLinearWithAsyncCommunication(torch.autograd.Function):
         ctx.async_grad_allreduce = async_grad_allreduce
         ctx.sp = sequence_parallel_enabled
         ctx.q_local, ctx.kv_local, ctx.kv_mult = q_local, kv_local, kv_mult
-        total_input = _gather_along_first_dim(input) if sequence_parallel_enabled else input
+        if sequence_parallel_enabled:
+            out, total_input = sp.gather_linear(input, weight)   # chunk-pipelined all-gather + GEMM
+        else:
+            total_input = input
+            out = _gemm.linear(total_input, weight)
         ctx.saved_gathered = (not sequence_parallel_enabled) or _SAVE_GATHERED_INPUT
         ctx.save_for_backward(total_input if ctx.saved_gathered else input, weight, bias)
-        out = torch.matmul(total_input, weight.t())
         if bias is not None:
             out = out + bias
         return out
@@ -102,18 +107,18 @@ class GQAQKVLinearWithAsyncCommunication(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_output):
         inp, weight, bias = ctx.saved_tensors
-        total_input = inp if ctx.saved_gathered else _gather_along_first_dim(inp)
+        total_input = inp if ctx.saved_gathered else sp.sp_gather(inp)
         grad_output = grad_output.contiguous()
-        grad_input = torch.matmul(grad_output, weight)
         group = get_tensor_model_parallel_group() if model_parallel_is_initialized() else None
         ws = dist.get_world_size(group=group) if group is not None else 1
-        handle, sub = None, None
+        handles = []
         if ctx.sp and ws > 1:
-            sub = torch.empty((grad_input.shape[0] // ws,) + tuple(grad_input.shape[1:]), dtype=grad_input.dtype,
-                              device=grad_input.device)
-            handle = comm.reduce_scatter_tensor(sub, grad_input.contiguous(), group=group, async_op=True)
-        elif ctx.async_grad_allreduce and ws > 1:
-            handle = dist.all_reduce(grad_input, group=group, async_op=True)
+            # dgrad GEMM chunks with their reduce-scatters in flight behind them
+            grad_input, handles = sp.matmul_reduce_scatter_start(grad_output, weight, group)
+        else:
+            grad_input = _gemm.matmul(grad_output, weight)
+            if ctx.async_grad_allreduce and ws > 1:
+                handles = [dist.all_reduce(grad_input, group=group, async_op=True)]
         go2 = grad_output.reshape(-1, grad_output.shape[-1])
         if ctx.kv_mult > 1 and _KV_SHARED_GROUP is not None:
             # sum the K/V output grads over the replicas before the weight-gradient GEMM
@@ -123,10 +128,9 @@ class GQAQKVLinearWithAsyncCommunication(torch.autograd.Function):
         x2 = total_input.reshape(-1, total_input.shape[-1])
         grad_weight = _accumulate_wgrad(weight, go2, x2)
         grad_bias = _bias_grad(bias, go2) if ctx.use_bias else None
-        if handle is not None:
-            handle.wait()
-        gi = sub if (ctx.sp and ws > 1) else grad_input
-        return gi, grad_weight, grad_bias, None, None, None, None, None
+        for h in handles:
+            h.wait()
+        return grad_input, grad_weight, grad_bias, None, None, None, None, None
 
 
 def gqa_qkv_linear_with_async_allreduce(input, weight, bias, q_local, kv_local, async_grad_allreduce,

@@ -32,6 +32,8 @@ from torch import nn
 from torch.nn.parameter import Parameter
 
 from .. import ops
+from ..ops import gemm as _gemm
+from . import sp
 from .mappings import (
     _gather_along_first_dim,
     copy_to_tensor_model_parallel_region,
@@ -88,10 +90,7 @@ def _accumulate_wgrad(weight: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor)
     mg = getattr(weight, "main_grad", None)
     if mg is None:
         return go2.t().matmul(x2)
-    if go2.is_cuda:
-        torch.addmm(mg, go2.t(), x2, out_dtype=torch.float32, out=mg)
-    else:
-        mg.add_(go2.t().float().matmul(x2.float()))
+    _gemm.wgrad_accumulate_(mg, go2, x2)
     _notify(weight)
     return None
 
@@ -109,7 +108,11 @@ def _bias_grad(bias, go2):
 
 
 class LinearWithAsyncCommunication(torch.autograd.Function):
-    """Y = X W^T (+ b) with the column-parallel input collectives fused into fwd/bwd."""
+    """Y = X W^T (+ b) with the column-parallel input collectives fused into fwd/bwd.
+
+    Sequence parallel: the input all-gather is chunk-pipelined with the GEMM (sp.gather_linear)
+    and the backward input-gradient reduce-scatter is chunk-pipelined with the dgrad GEMM and
+    overlapped with the weight-gradient GEMM (sp.matmul_reduce_scatter_start)."""
 
     @staticmethod
     def forward(ctx, input, weight, bias, async_grad_allreduce, sequence_parallel_enabled, save_for_backward=True,
@@ -119,14 +122,14 @@ class LinearWithAsyncCommunication(torch.autograd.Function):
         ctx.sequence_parallel_enabled = sequence_parallel_enabled
         ctx.process_group = process_group
         if sequence_parallel_enabled:
-            total_input = _gather_along_first_dim(input)
+            output, total_input = sp.gather_linear(input, weight, process_group)
         else:
             total_input = input
+            output = _gemm.linear(total_input, weight)
         ctx.saved_gathered = sequence_parallel_enabled and _SAVE_GATHERED_INPUT
         if save_for_backward:
             ctx.save_for_backward(total_input if (ctx.saved_gathered or not sequence_parallel_enabled) else input, weight,
                                   bias)
-        output = torch.matmul(total_input, weight.t())
         if bias is not None:
             output = output + bias
         return output
@@ -135,34 +138,49 @@ class LinearWithAsyncCommunication(torch.autograd.Function):
     def backward(ctx, grad_output):
         inp, weight, bias = ctx.saved_tensors
         if ctx.sequence_parallel_enabled and not ctx.saved_gathered:
-            total_input = _gather_along_first_dim(inp)
+            total_input = sp.sp_gather(inp, ctx.process_group)
         else:
             total_input = inp
         grad_output = grad_output.contiguous()
-        grad_input = torch.matmul(grad_output, weight)
         group = ctx.process_group if ctx.process_group is not None else get_tensor_model_parallel_group()
-        handle = None
-        sub_grad_input = None
-        if ctx.sequence_parallel_enabled:
-            ws = dist.get_world_size(group=group)
-            if ws > 1:
-                shape = (grad_input.shape[0] // ws,) + tuple(grad_input.shape[1:])
-                sub_grad_input = torch.empty(shape, dtype=grad_input.dtype, device=grad_input.device)
-                handle = comm.reduce_scatter_tensor(sub_grad_input, grad_input.contiguous(), group=group, async_op=True)
-            else:
-                sub_grad_input = grad_input
-        elif ctx.async_grad_allreduce and dist.get_world_size(group=group) > 1:
-            grad_input = grad_input.contiguous()
-            handle = dist.all_reduce(grad_input, group=group, async_op=True)
+        handles = []
+        if ctx.sequence_parallel_enabled and dist.get_world_size(group=group) > 1:
+            grad_input, handles = sp.matmul_reduce_scatter_start(grad_output, weight, group)
+        else:
+            grad_input = _gemm.matmul(grad_output, weight)
+            if not ctx.sequence_parallel_enabled and ctx.async_grad_allreduce and dist.get_world_size(group=group) > 1:
+                handles = [dist.all_reduce(grad_input, group=group, async_op=True)]
         go2 = grad_output.reshape(-1, grad_output.shape[-1])
         x2 = total_input.reshape(-1, total_input.shape[-1])
         grad_weight = _accumulate_wgrad(weight, go2, x2)
         grad_bias = _bias_grad(bias, go2) if ctx.use_bias else None
-        if handle is not None:
-            handle.wait()
-        if ctx.sequence_parallel_enabled:
-            return sub_grad_input, grad_weight, grad_bias, None, None, None, None
+        for h in handles:
+            h.wait()
         return grad_input, grad_weight, grad_bias, None, None, None, None
+
+
+class RowParallelSPLinear(torch.autograd.Function):
+    """Row-parallel linear with sequence parallelism: reduce_scatter(X W^T), the reduce-scatter of
+    each sequence chunk overlapping the GEMM of the next; backward all-gathers the output grad
+    chunk-pipelined with the dgrad GEMM."""
+
+    @staticmethod
+    def forward(ctx, input, weight, process_group=None):
+        ctx.process_group = process_group
+        local, hs = sp.linear_reduce_scatter_start(input, weight, process_group)
+        ctx.save_for_backward(input, weight)
+        for h in hs:
+            h.wait()
+        return local
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        inp, weight = ctx.saved_tensors
+        grad_input, g_full = sp.gather_matmul(grad_output.contiguous(), weight, ctx.process_group)
+        go2 = g_full.reshape(-1, g_full.shape[-1])
+        x2 = inp.reshape(-1, inp.shape[-1])
+        grad_weight = _accumulate_wgrad(weight, go2, x2)
+        return grad_input, grad_weight, None
 
 
 def linear_with_async_allreduce(input, weight, bias, async_grad_allreduce, sequence_parallel_enabled,
@@ -341,11 +359,16 @@ class RowParallelLinear(BaseParallelLinear):
                 input_ = F.pad(input_, (0, self.pad_size))
             assert not self.sequence_parallel_enabled
             input_parallel = scatter_to_tensor_model_parallel_region(input_)
-        output_parallel = self._forward_impl(input_parallel, self.weight, None, False, False, self.autograd_func_class)
-        if self.sequence_parallel_enabled:
-            output_ = reduce_scatter_to_sequence_parallel_region(output_parallel)
+        if self.sequence_parallel_enabled and get_tensor_model_parallel_size() > 1 and \
+                self.autograd_func_class is LinearWithAsyncCommunication:
+            output_ = RowParallelSPLinear.apply(input_parallel, self.weight, None)
         else:
-            output_ = reduce_from_tensor_model_parallel_region(output_parallel)
+            output_parallel = self._forward_impl(input_parallel, self.weight, None, False, False,
+                                                 self.autograd_func_class)
+            if self.sequence_parallel_enabled:
+                output_ = reduce_scatter_to_sequence_parallel_region(output_parallel)
+            else:
+                output_ = reduce_from_tensor_model_parallel_region(output_parallel)
         if self.skip_bias_add:
             return output_, self.bias
         return output_ + self.bias if self.bias is not None else output_

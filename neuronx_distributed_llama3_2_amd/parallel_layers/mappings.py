@@ -23,6 +23,7 @@ from .parallel_state import (
     get_tensor_model_parallel_rank,
     get_tensor_model_parallel_size,
 )
+from .sp import sp_gather, sp_reduce_scatter, sp_split
 from .utils import split_tensor_along_dim
 
 
@@ -177,13 +178,15 @@ class _GatherFromModelParallelRegion(torch.autograd.Function):
 
 
 class _ScatterToSequenceParallelRegion(torch.autograd.Function):
+    """Split along the sequence into this rank's (chunk-interleaved, see sp.py) SP shard."""
+
     @staticmethod
     def forward(ctx, input_):
-        return _split_along_first_dim(input_)
+        return sp_split(input_)
 
     @staticmethod
     def backward(ctx, grad_output):
-        return _gather_along_first_dim(grad_output)
+        return sp_gather(grad_output)
 
 
 class _GatherFromSequenceParallelRegion(torch.autograd.Function):
@@ -193,23 +196,23 @@ class _GatherFromSequenceParallelRegion(torch.autograd.Function):
     @staticmethod
     def forward(ctx, input_, to_model_parallel=True):
         ctx.to_model_parallel = to_model_parallel
-        return _gather_along_first_dim(input_)
+        return sp_gather(input_)
 
     @staticmethod
     def backward(ctx, grad_output):
         if ctx.to_model_parallel:
-            return _reduce_scatter_along_first_dim(grad_output), None
-        return _split_along_first_dim(grad_output), None
+            return sp_reduce_scatter(grad_output), None
+        return sp_split(grad_output), None
 
 
 class _ReduceScatterToSequenceParallelRegion(torch.autograd.Function):
     @staticmethod
     def forward(ctx, input_):
-        return _reduce_scatter_along_first_dim(input_)
+        return sp_reduce_scatter(input_)
 
     @staticmethod
     def backward(ctx, grad_output):
-        return _gather_along_first_dim(grad_output)
+        return sp_gather(grad_output)
 
 
 class _ReduceScatterToTensorParallelRegionWithDim(torch.autograd.Function):

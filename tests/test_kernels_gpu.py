@@ -240,3 +240,23 @@ def test_sampling():
     assert torch.equal(idx, ri)
     rt = ops.topk_sample(x.cpu(), 50, 1.0, u.cpu())
     assert torch.equal(tok.cpu(), rt)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 384, 512), (1, 1000, 512), (8192, 1024, 4096)])
+def test_tuned_gemm_variants(M, N, K):
+    from neuronx_distributed_llama3_2_amd.ops import gemm
+
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    ref = x.float() @ w.float().t()
+    y = gemm.linear(x, w)
+    torch.testing.assert_close(y.float(), ref, atol=2e-2 * ref.abs().max().item(), rtol=2e-2)
+    g = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    dx = gemm.matmul(g, w)
+    torch.testing.assert_close(dx.float(), g.float() @ w.float(), atol=2e-2 * (g.float() @ w.float()).abs().max().item(),
+                               rtol=2e-2)
+    mg = torch.randn(N, K, device="cuda", dtype=torch.float32)
+    exp = mg + g.float().t() @ x.float()
+    gemm.wgrad_accumulate_(mg, g, x)
+    torch.testing.assert_close(mg, exp, atol=1e-3 * exp.abs().max().item(), rtol=1e-3)
