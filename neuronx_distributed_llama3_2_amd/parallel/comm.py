@@ -40,8 +40,9 @@ def all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, asy
         return dist.all_gather_into_tensor(out, inp.contiguous(), group=group, async_op=async_op)
     ws = dist.get_world_size(group=group)
     chunks = list(out.chunk(ws, dim=0))
-    tmp = [torch.empty_like(inp) for _ in range(ws)]
-    dist.all_gather(tmp, inp.contiguous(), group=group)
+    src = inp.detach().contiguous().cpu()   # gloo gathers host tensors (GPU tensors are staged)
+    tmp = [torch.empty_like(src) for _ in range(ws)]
+    dist.all_gather(tmp, src, group=group)
     for c, t in zip(chunks, tmp):
         c.copy_(t)
     return _Done() if async_op else None
@@ -80,7 +81,7 @@ def _a2a_via_gather(outs: List[torch.Tensor], ins: List[torch.Tensor], group):
     """gloo has no all_to_all: every rank all-gathers the stacked chunks and keeps its column."""
     ws = dist.get_world_size(group=group)
     r = dist.get_rank(group=group)
-    stacked = torch.stack(ins)
+    stacked = torch.stack(ins).cpu()
     gathered = [torch.empty_like(stacked) for _ in range(ws)]
     dist.all_gather(gathered, stacked, group=group)
     for src in range(ws):
