@@ -95,6 +95,14 @@ class ExpertMLPs(nn.Module):
                               device=device, input_layer_init_method=init_method,
                               output_layer_init_method=output_layer_init_method)
         self.dtype, self.device = dtype, device
+        self.input_grad_reduced_by_caller = False
+
+    def set_input_grad_reduced_by_caller(self, flag: bool = True) -> None:
+        """The MoE layer reduces the (TP-partial) input gradient once for router + experts."""
+        self.input_grad_reduced_by_caller = flag
+        self.mlp_op.gate_up_proj.async_tensor_model_parallel_allreduce = \
+            (not flag) and ps.get_tensor_model_parallel_size() > 1
+        self.mlp_op.gate_up_proj.skip_input_copy = flag
 
     # ------------------------------------------------------------------ helpers
     def get_expert_mask(self, expert_index: torch.Tensor) -> torch.Tensor:
@@ -122,7 +130,7 @@ class ExpertMLPs(nn.Module):
             raise NotImplementedError("Expert parallelism requires a capacity factor (static all-to-all shapes)")
         T, H = hidden_states.shape
         k = self.top_k
-        if ps.get_tensor_model_parallel_size() > 1:
+        if ps.get_tensor_model_parallel_size() > 1 and not self.input_grad_reduced_by_caller:
             # experts are TP-sharded on I: input grads are partial sums over TP
             hidden_states = copy_to_tensor_model_parallel_region(hidden_states)
         flat_e = expert_index.reshape(-1)                      # [T*k]
@@ -159,7 +167,8 @@ class ExpertMLPs(nn.Module):
     def forward_capacity_factor(self, hidden_states, expert_affinities, expert_index):
         T, H = hidden_states.shape
         E, k = self.num_experts, self.top_k
-        C = min(T, math.ceil(T * k * self.capacity_factor / E))
+        cf = self.capacity_factor if self.capacity_factor is not None else E / k   # None: full capacity
+        C = min(T, math.ceil(T * k * cf / E))
         mask = self.get_expert_mask(expert_index)              # [T, E]
         pos = cumsum(mask)                                     # 1-based position in expert
         mask = mask.masked_fill(pos > C, 0)
@@ -194,6 +203,9 @@ class ExpertMLPs(nn.Module):
         return torch.stack(outs, 0)
 
     def forward(self, hidden_states, expert_affinities, expert_index, seq_len: int):
+        if ps.get_expert_model_parallel_size() > 1:
+            # the EP all-to-all needs static per-expert capacity (full capacity when cf is None)
+            return self.forward_capacity_factor(hidden_states, expert_affinities, expert_index)
         if self.training:
             if self.capacity_factor is None:
                 return self.forward_dropless(hidden_states, expert_affinities, expert_index)

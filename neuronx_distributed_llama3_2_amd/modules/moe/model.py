@@ -29,13 +29,21 @@ class MoE(torch.nn.Module):
         self.sequence_parallel_enabled = sequence_parallel_enabled
         self.return_router_logits = return_router_logits
         self.ep_enabled = ps.get_expert_model_parallel_size() > 1
+        if ps.get_tensor_model_parallel_size() > 1:
+            # router + experts both see TP-partial gradients: reduce the input grad ONCE here
+            self.expert_mlps.set_input_grad_reduced_by_caller(True)
+            self.router.linear_router.reduce_weight_grad = True
 
     def forward(self, hidden_states: torch.Tensor):
         if not self.training:
             assert not self.sequence_parallel_enabled, "SP is not currently supported for inference"
         sp = self.sequence_parallel_enabled and ps.get_tensor_model_parallel_size() > 1
-        full = mappings.gather_from_sequence_parallel_region(hidden_states, to_model_parallel=False) if sp \
-            else hidden_states
+        if sp:   # backward: reduce-scatter of the TP-partial input grads
+            full = mappings.gather_from_sequence_parallel_region(hidden_states, to_model_parallel=True)
+        elif ps.get_tensor_model_parallel_size() > 1:
+            full = mappings.copy_to_tensor_model_parallel_region(hidden_states)
+        else:
+            full = hidden_states
         shape = full.shape
         seq_len = shape[0] if self.training else shape[1]
         x = full.reshape(-1, shape[-1])

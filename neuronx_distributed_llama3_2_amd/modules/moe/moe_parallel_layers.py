@@ -122,9 +122,11 @@ class ExpertFusedColumnParallelLinear(_ExpertFusedBase):
         self.input_size, self.output_size, self.stride = input_size, output_size, stride
         self._create(num_experts, input_size, output_size, 2, stride, init_method, dtype, device, output_size)
         self.async_tensor_model_parallel_allreduce = ps.get_tensor_model_parallel_size() > 1
+        self.skip_input_copy = False
 
     def forward(self, input_: torch.Tensor, expert_indices: Optional[torch.Tensor] = None) -> torch.Tensor:
-        x = input_ if self.async_tensor_model_parallel_allreduce else copy_to_tensor_model_parallel_region(input_)
+        x = input_ if (self.async_tensor_model_parallel_allreduce or self.skip_input_copy) \
+            else copy_to_tensor_model_parallel_region(input_)
         w = self.weight[expert_indices] if expert_indices is not None else self.weight
         return ExpertFusedLinearWithAsyncCommunication.apply(x, w, None, self.async_tensor_model_parallel_allreduce,
                                                              False)
@@ -172,16 +174,18 @@ class LinearWithWeightGradAR(torch.autograd.Function):
 
 
 class LinearRouter(nn.Module):
-    """Replicated router projection [E, H] (fp32 by default)."""
+    """Replicated router projection [E, H] (fp32 by default).  Inside a TP MoE layer the logits'
+    gradients are TP-partial (each rank combines only its shard of every expert's output), so the
+    weight gradient is all-reduced over TP (`reduce_weight_grad`, set by the MoE layer)."""
 
     def __init__(self, input_size: int, output_size: int, sequence_parallel_enabled: bool = False,
                  dtype: torch.dtype = torch.float32, device: Optional[torch.device] = None):
         super().__init__()
         self.input_size, self.output_size = input_size, output_size
         self.sequence_parallel_enabled = sequence_parallel_enabled
+        self.reduce_weight_grad = sequence_parallel_enabled
         device = torch.device(device) if device is not None else torch.device("cpu")
         self.weight = Parameter(torch.empty(output_size, input_size, dtype=dtype, device=device))
-        setattr(self.weight, "sequence_parallel_enabled", sequence_parallel_enabled)
         if device.type != "meta":
             self.init_weight_cpu()
 
@@ -190,4 +194,4 @@ class LinearRouter(nn.Module):
 
     def forward(self, input_):
         x = input_.to(self.weight.dtype)
-        return LinearWithWeightGradAR.apply(x, self.weight, self.sequence_parallel_enabled)
+        return LinearWithWeightGradAR.apply(x, self.weight, self.reduce_weight_grad)

@@ -1,0 +1,194 @@
+"""MoE: dispatch-mode equivalence, capacity dropping, routers, TP / EP parity on gloo
+(reference tests: test/unit_test/modules/moe/*, test/integration/modules/moe/test_moe_*)."""
+
+import os
+import tempfile
+
+import pytest
+import torch
+
+from dist_utils import run_distributed
+from neuronx_distributed_llama3_2_amd.parallel_layers import parallel_state as ps
+
+
+def _single():
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29633")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    if not ps.model_parallel_is_initialized():
+        ps.initialize_model_parallel(1)
+
+
+def _layer(E=4, k=2, H=32, I=48, cf=None, sp=False, seed=0, router="topk", normalize=True):
+    from neuronx_distributed_llama3_2_amd.modules.moe import MoE, ExpertMLPs, RouterSinkhorn, RouterTopK
+
+    torch.manual_seed(seed)
+    r = RouterTopK(E, k, H) if router == "topk" else RouterSinkhorn(E, 1, H)
+    torch.manual_seed(seed + 1)
+    mlps = ExpertMLPs(E, k, H, I, "silu", True, cf, normalize_top_k_affinities=normalize and k > 1)
+    return MoE(r, mlps, sequence_parallel_enabled=sp, return_router_logits=True)
+
+
+def _dense_reference(layer, x):
+    """Per-token loop over the chosen experts (fp32, no dispatch tricks)."""
+    m = layer.expert_mlps
+    logits = x @ layer.router.linear_router.weight.t()
+    aff = torch.softmax(logits.float(), -1)
+    idx = torch.topk(logits, m.top_k).indices
+    ch = aff.gather(1, idx)
+    if m.normalize_top_k_affinities:
+        ch = ch / ch.sum(1, keepdim=True)
+    wgu, wd = m.mlp_op.gate_up_proj.weight, m.mlp_op.down_proj.weight
+    out = torch.zeros_like(x)
+    for t in range(x.shape[0]):
+        for j in range(m.top_k):
+            e = int(idx[t, j])
+            gu = x[t] @ wgu[e]
+            g, u = gu.chunk(2)
+            out[t] += ch[t, j] * ((torch.nn.functional.silu(g) * u) @ wd[e])
+    return out
+
+
+def test_dispatch_modes_match_dense_reference():
+    _single()
+    layer = _layer()
+    x = torch.randn(24, 1, 32)
+    ref = _dense_reference(layer, x.view(24, 32)).view(24, 1, 32)
+    layer.train()
+    out_dropless, logits = layer(x)
+    torch.testing.assert_close(out_dropless, ref, atol=1e-5, rtol=1e-5)
+    layer.expert_mlps.capacity_factor = 1e9 / 1e9 * 2.0  # E/top_k = 2 -> full capacity but via the CF path
+    out_cf, _ = layer(x)
+    torch.testing.assert_close(out_cf, ref, atol=1e-5, rtol=1e-5)
+    y = layer.expert_mlps.forward_all_experts(x.view(24, 32), *layer.router(x.view(24, 32))[1:])
+    torch.testing.assert_close(y.view(24, 1, 32), ref, atol=1e-5, rtol=1e-5)
+    layer.eval()
+    layer.expert_mlps.capacity_factor = None
+    xs = x[:1].transpose(0, 1)  # [B=1, S=1, H] token generation -> selective loading
+    out_sel, _ = layer(xs)
+    torch.testing.assert_close(out_sel.view(32), ref[0, 0], atol=1e-5, rtol=1e-5)
+
+
+def test_capacity_factor_drops_late_tokens():
+    _single()
+    layer = _layer(E=4, k=1, cf=0.5, normalize=False)
+    layer.train()
+    x = torch.randn(16, 1, 32)
+    out, _ = layer(x)
+    T = 16
+    C = max(1, -(-T * 1 * 0.5 // 4))
+    idx = torch.topk(x.view(T, 32) @ layer.router.linear_router.weight.t(), 1).indices.view(-1)
+    seen = {}
+    for t in range(T):
+        e = int(idx[t])
+        seen[e] = seen.get(e, 0) + 1
+        if seen[e] > C:
+            assert torch.all(out[t] == 0), f"token {t} should have been dropped"
+        else:
+            assert out[t].abs().sum() > 0
+
+
+def test_sinkhorn_router_and_balancing_loss():
+    _single()
+    from neuronx_distributed_llama3_2_amd.modules.moe import RouterSinkhorn, load_balancing_loss_func
+
+    torch.manual_seed(0)
+    r = RouterSinkhorn(4, 1, 16)
+    x = torch.randn(64, 16) + 3 * torch.randn(1, 16)  # strongly biased tokens
+    r.train()
+    _, aff, idx = r(x)
+    counts = torch.bincount(idx.view(-1), minlength=4)
+    assert counts.max() <= 32, counts  # balanced far better than argmax of biased logits
+    logits = torch.randn(100, 8)
+    loss = load_balancing_loss_func(logits, 8, 2)
+    p = torch.softmax(logits, -1)
+    sel = torch.topk(p, 2).indices
+    f = torch.nn.functional.one_hot(sel, 8).float().mean(0)
+    torch.testing.assert_close(loss, (f * p.mean(0)).sum() * 4)
+
+
+def _w_tp(rank, world, tp, ep, sp, cf, out):
+    ps.initialize_model_parallel(tensor_model_parallel_size=tp, expert_model_parallel_size=ep)
+    layer = _layer(E=4, k=2, cf=cf, sp=sp, seed=3)
+    layer.train()
+    torch.manual_seed(11)
+    x_full = torch.randn(32, 2, 32)
+    if sp:
+        from neuronx_distributed_llama3_2_amd.parallel_layers.sp import sp_split
+
+        x = sp_split(x_full).requires_grad_(True)
+    else:
+        x = x_full.clone().requires_grad_(True)
+    y, logits = layer(x)
+    (y.float() ** 2).sum().backward()
+    if sp:
+        from neuronx_distributed_llama3_2_amd.parallel_layers.sp import sp_gather
+
+        y = sp_gather(y.detach())
+        gx = sp_gather(x.grad)
+    else:
+        gx = x.grad
+    if rank == 0:
+        torch.save({"y": y.detach(), "gx": gx}, out)
+
+
+@pytest.mark.parametrize("sp", [False, True])
+def test_moe_tp2_matches_tp1(sp):
+    d = tempfile.mkdtemp()
+    run_distributed(_w_tp, 1, 1, 1, False, None, os.path.join(d, "a.pt"))
+    run_distributed(_w_tp, 2, 2, 1, sp, None, os.path.join(d, "b.pt"))
+    a, b = torch.load(os.path.join(d, "a.pt")), torch.load(os.path.join(d, "b.pt"))
+    torch.testing.assert_close(a["y"], b["y"], atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(a["gx"], b["gx"], atol=1e-5, rtol=1e-4)
+
+
+def test_moe_ep2_capacity_matches_ep1():
+    d = tempfile.mkdtemp()
+    run_distributed(_w_tp, 1, 1, 1, False, 1.0, os.path.join(d, "a.pt"))
+    run_distributed(_w_tp, 2, 1, 2, False, 1.0, os.path.join(d, "b.pt"))
+    a, b = torch.load(os.path.join(d, "a.pt")), torch.load(os.path.join(d, "b.pt"))
+    torch.testing.assert_close(a["y"], b["y"], atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(a["gx"], b["gx"], atol=1e-5, rtol=1e-4)
+
+
+def _w_mixtral(rank, world, tp, ep, sp, cf, out):
+    import neuronx_distributed_llama3_2_amd as nxd
+    from neuronx_distributed_llama3_2_amd.models.mixtral import MixtralForCausalLM, mixtral_config
+
+    cfg_nxd = nxd.neuronx_distributed_config(tensor_parallel_size=tp, expert_parallel_size=ep,
+                                            optimizer_config={"zero_one_enabled": True, "grad_clipping": True,
+                                                              "max_grad_norm": 1.0})
+    cfg = mixtral_config("tiny", sequence_parallel_enabled=sp, capacity_factor=cf)
+    torch.manual_seed(0)
+    model = nxd.initialize_parallel_model(cfg_nxd, MixtralForCausalLM, cfg, torch.float32)
+    opt = nxd.initialize_parallel_optimizer(cfg_nxd, torch.optim.AdamW, model.parameters(), lr=3e-3)
+    g = torch.Generator().manual_seed(3)
+    batch = torch.randint(0, cfg.vocab_size, (4, 32), generator=g)
+    dp, dpr = ps.get_data_parallel_size(), ps.get_data_parallel_rank()
+    losses = []
+    for _ in range(4):
+        local = batch.chunk(dp)[dpr]
+        o = model(local, labels=local)
+        o.loss.backward()
+        opt.step()
+        opt.zero_grad()
+        l = o.loss.detach().clone()
+        torch.distributed.all_reduce(l)
+        losses.append(float(l) / world)
+    if rank == 0:
+        torch.save(losses, out)
+
+
+def test_mixtral_trains_tp_ep():
+    """tiny Mixtral: TP=2+SP (dropless) and EP=2 (capacity factor) train; TP run matches TP=1."""
+    d = tempfile.mkdtemp()
+    run_distributed(_w_mixtral, 1, 1, 1, False, None, os.path.join(d, "a.pt"))
+    run_distributed(_w_mixtral, 2, 2, 1, True, None, os.path.join(d, "b.pt"))
+    run_distributed(_w_mixtral, 2, 1, 2, False, 2.0, os.path.join(d, "c.pt"))
+    a, b, c = (torch.load(os.path.join(d, f)) for f in ("a.pt", "b.pt", "c.pt"))
+    assert a[-1] < a[0] and b[-1] < b[0] and c[-1] < c[0], (a, b, c)
+    for x, y in zip(a, b):
+        assert abs(x - y) < 2e-3 * abs(x), (a, b)
