@@ -126,7 +126,7 @@ class GQAQKVLinearWithAsyncCommunication(torch.autograd.Function):
             dist.all_reduce(kv, group=_KV_SHARED_GROUP)
             go2 = torch.cat([go2[:, :ctx.q_local], kv], dim=1)
         x2 = total_input.reshape(-1, total_input.shape[-1])
-        grad_weight = _accumulate_wgrad(weight, go2, x2)
+        grad_weight = _accumulate_wgrad(weight, go2, x2) if ctx.needs_input_grad[1] else None
         grad_bias = _bias_grad(bias, go2) if ctx.use_bias else None
         for h in handles:
             h.wait()

@@ -152,7 +152,7 @@ class LinearWithAsyncCommunication(torch.autograd.Function):
                 handles = [dist.all_reduce(grad_input, group=group, async_op=True)]
         go2 = grad_output.reshape(-1, grad_output.shape[-1])
         x2 = total_input.reshape(-1, total_input.shape[-1])
-        grad_weight = _accumulate_wgrad(weight, go2, x2)
+        grad_weight = _accumulate_wgrad(weight, go2, x2) if ctx.needs_input_grad[1] else None
         grad_bias = _bias_grad(bias, go2) if ctx.use_bias else None
         for h in handles:
             h.wait()
@@ -179,7 +179,7 @@ class RowParallelSPLinear(torch.autograd.Function):
         grad_input, g_full = sp.gather_matmul(grad_output.contiguous(), weight, ctx.process_group)
         go2 = g_full.reshape(-1, g_full.shape[-1])
         x2 = inp.reshape(-1, inp.shape[-1])
-        grad_weight = _accumulate_wgrad(weight, go2, x2)
+        grad_weight = _accumulate_wgrad(weight, go2, x2) if ctx.needs_input_grad[1] else None
         return grad_input, grad_weight, None
 
 
