@@ -38,6 +38,9 @@ int kv_cache_write_launch(const void*, const void*, const int64_t*, void*, void*
 int argmax_launch(const void*, int, int64_t, int, int, int64_t*, hipStream_t);
 int topk_sample_launch(const void*, int, int64_t, int, int, int, float, const float*, int64_t*, float*, int64_t*,
                        hipStream_t);
+int gemv_launch(const void*, int64_t, const void*, int64_t, int, const float*, float, const void*, void*, int64_t, int, int,
+                int, int, hipStream_t);
+int dequant_int8_launch(const void*, int64_t, const float*, float, void*, int, int, hipStream_t);
 }  // namespace nxd
 
 namespace {
@@ -441,12 +444,66 @@ void topk_sample(at::Tensor x, int64_t k, double temperature, c10::optional<at::
            "topk_sample");
 }
 
+// y[M, N] = x[M, K] @ W^T (W bf16 or int8 [Nw, K], Nw = N or 2N with glu), optional per-row fp32
+// scale / per-tensor scale, optional bias [Nw]; M <= 8.
+void gemv(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> scale, double tscale, c10::optional<at::Tensor> bias,
+          at::Tensor y, bool glu) {
+  check_cuda(x, "x");
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "gemv: 2-D operands");
+  TORCH_CHECK(x.stride(1) == 1 && w.stride(1) == 1 && y.stride(1) == 1, "gemv: unit inner strides required");
+  const bool i8 = w.scalar_type() == at::kChar;
+  TORCH_CHECK(i8 || w.scalar_type() == at::kBFloat16, "gemv: weight must be bf16 or int8");
+  const int M = x.size(0), K = x.size(1), N = y.size(1);
+  TORCH_CHECK(M >= 1 && M <= 8 && y.size(0) == M, "gemv: 1 <= M <= 8");
+  TORCH_CHECK(w.size(1) == K && w.size(0) == (glu ? 2 * N : N), "gemv: weight shape mismatch");
+  const int epl = i8 ? 16 : 8;
+  TORCH_CHECK(K % epl == 0 && x.stride(0) % 8 == 0 && w.stride(0) % epl == 0, "gemv: K / leading dims must be multiples of ",
+              epl);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "gemv: 16-byte aligned operands required");
+  const float* sp = nullptr;
+  if (scale.has_value()) {
+    TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->is_contiguous() && scale->numel() == w.size(0),
+                "gemv: scale must be fp32 [Nw]");
+    sp = scale->data_ptr<float>();
+  }
+  const void* bp = nullptr;
+  if (bias.has_value()) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == w.size(0), "gemv: bias must be [Nw]");
+    bp = bias->data_ptr();
+  }
+  check_rc(nxd::gemv_launch(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), i8, sp, (float)tscale, bp,
+                            y.data_ptr(), y.stride(0), M, N, K, glu, cur_stream()),
+           "gemv");
+}
+
+void dequant_int8(at::Tensor w, c10::optional<at::Tensor> scale, double tscale, at::Tensor out) {
+  check_cuda(w, "w");
+  TORCH_CHECK(w.scalar_type() == at::kChar && w.dim() == 2 && w.stride(1) == 1, "dequant: int8 [N, K] weight");
+  check_bf16(out, "out");
+  TORCH_CHECK(out.is_contiguous() && out.sizes() == w.sizes(), "dequant: out must be contiguous [N, K]");
+  const int N = w.size(0), K = w.size(1);
+  TORCH_CHECK(K % 16 == 0 && w.stride(0) % 16 == 0, "dequant: K must be a multiple of 16");
+  const float* sp = nullptr;
+  if (scale.has_value()) {
+    TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->is_contiguous() && scale->numel() == N, "dequant: scale [N]");
+    sp = scale->data_ptr<float>();
+  }
+  check_rc(nxd::dequant_int8_launch(w.data_ptr(), w.stride(0), sp, (float)tscale, out.data_ptr(), N, K, cur_stream()),
+           "dequant_int8");
+}
+
 }  // namespace
 
 void register_gemm(pybind11::module& m);  // gemm.cpp
 
 PYBIND11_MODULE(_C, m) {
   register_gemm(m);
+  m.def("gemv", &gemv);
+  m.def("dequant_int8", &dequant_int8);
   m.doc() = "CDNA4 (gfx950) kernels of neuronx_distributed_llama3_2_amd";
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);

@@ -108,6 +108,8 @@ class LlamaForCausalLMInference:
                 ps.initialize_model_parallel(tensor_model_parallel_size=1)
         self.model = LlamaInferenceModel(model_config, dtype=dtype,
                                          device=torch.device("meta") if not init_weights else self.device)
+        if config.quantized:
+            self._quantize()
         self.max_batch = config.max_batch_size
         self.graph_steps = max(1, int(config.decode_graph_steps))
         # KV-cache slack so a final multi-step replay may overshoot max_length without faulting
@@ -119,6 +121,15 @@ class LlamaForCausalLMInference:
         self.token_generation_model = _SubModel(self, TOKEN_GENERATION_MODEL)
         if init_weights:
             self.model.setup_kv_cache(self.max_batch, self.cache_len, self.device)
+
+    def _quantize(self) -> None:
+        """Swap the decoder / lm_head linears for int8 weight-only layers (reference flow:
+        run_llama_quantized.py -> quantize_pytorch_model_per_*_symmetric + convert)."""
+        from ..quantization import convert, get_default_custom_qconfig_dict, get_default_per_channel_custom_qconfig_dict
+
+        qt = str(self.config.quantization_type)
+        q = get_default_per_channel_custom_qconfig_dict() if "channel" in qt else get_default_custom_qconfig_dict()
+        convert(self.model, q, inplace=True)
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -146,11 +157,17 @@ class LlamaForCausalLMInference:
     def _load_local(self, local: Dict[str, torch.Tensor]) -> None:
         if any(p.device.type == "meta" for p in self.model.parameters()):
             self.model.to_empty(device=self.device)
-            if getattr(self.model_config, "tie_word_embeddings", False):
+            if getattr(self.model_config, "tie_word_embeddings", False) and self.model.lm_head.weight.is_floating_point():
                 self.model.lm_head.weight = self.model.model.embed_tokens.weight
-        missing, unexpected = self.model.load_state_dict({k: v.to(self.dtype) for k, v in local.items()}, strict=False)
+        tied_q = getattr(self.model_config, "tie_word_embeddings", False) and \
+            not self.model.lm_head.weight.is_floating_point()
+        if tied_q and "lm_head.weight" not in local and "model.embed_tokens.weight" in local:
+            local["lm_head.weight"] = local["model.embed_tokens.weight"]   # quantized copy of the tied table
+        local = {k: (v.to(self.dtype) if v.is_floating_point() and k.split(".")[-1] != "scale" else v)
+                 for k, v in local.items()}
+        missing, unexpected = self.model.load_state_dict(local, strict=False)
         missing = [m for m in missing if not (getattr(self.model_config, "tie_word_embeddings", False)
-                                              and m == "lm_head.weight")]
+                                              and m == "lm_head.weight" and not tied_q)]
         if missing:
             raise RuntimeError(f"missing weights: {missing[:8]}")
         for p in self.model.parameters():

@@ -30,6 +30,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops.gemm import linear as _linear
+from ..ops.gemv import skinny_linear
 from ..models.llama.modeling_llama import LlamaForCausalLM
 from ..parallel_layers import parallel_state as ps
 from ..parallel_layers.parallel_state import get_tensor_model_parallel_size
@@ -100,8 +101,7 @@ class LlamaInferenceModel(LlamaForCausalLM):
         for i, layer in enumerate(self.model.layers):
             attn, mlp = layer.self_attn, layer.mlp
             h, residual = self._norm(x, layer.input_layernorm.weight, residual)
-            w_qkv, b_qkv = attn.qkv_proj._fused_weight_bias()
-            qkv = _linear(h, w_qkv, b_qkv)  # [B, T, W]
+            qkv = self._proj(attn.qkv_proj, h)  # [B, T, W]
             ops.rope_inplace_(qkv.view(B * T, W), 0, nq + nkv, D, cos_t, sin_t, pos_flat)
             q = qkv.view(B, T, nq + 2 * nkv, D)[:, :, :nq]
             k = qkv.view(B, T, nq + 2 * nkv, D)[:, :, nq:nq + nkv]
@@ -112,18 +112,40 @@ class LlamaInferenceModel(LlamaForCausalLM):
                 o, _ = ops.flash_attn_fwd_lse(q, k, v, causal=True)
             else:
                 o = ops.decode_attention(q, kc, vc, cache_len, seq_ids)
-            x = _linear(o.reshape(B, T, nq * D), attn.o_proj.weight, attn.o_proj.bias)
-            x = self._all_reduce(x)
+            x = self._row(attn.o_proj, o.reshape(B, T, nq * D))
             h, residual = self._norm(x, layer.post_attention_layernorm.weight, residual)
-            a = ops.swiglu(_linear(h, mlp.gate_up_proj.weight))
-            x = self._all_reduce(_linear(a, mlp.down_proj.weight))
+            a = self._proj(mlp.gate_up_proj, h, glu=True)   # SwiGLU fused into the decode GEMV
+            x = self._row(mlp.down_proj, a)
         if last_index is not None:
             rows = torch.arange(B, device=x.device)
             x = x[rows, last_index]
             residual = residual[rows, last_index]
         h, _ = self._norm(x, self.model.norm.weight, residual)
-        logits = _linear(h, self.lm_head.weight)
+        logits = self._proj(self.lm_head, h)
         return self._gather_vocab(logits)
+
+    def _row(self, mod, x: torch.Tensor) -> torch.Tensor:
+        """Row-parallel projection: partial GEMM, TP all-reduce, then the (replicated) bias."""
+        y = self._all_reduce(self._proj(mod, x, use_bias=False))
+        b = getattr(mod, "bias", None)
+        return y + b if b is not None else y
+
+    @staticmethod
+    def _proj(mod, x: torch.Tensor, glu: bool = False, use_bias: bool = True) -> torch.Tensor:
+        """Local (no-collective) projection of a TP linear: bf16 or int8-quantized weights; decode-sized
+        inputs go through the skinny-GEMM kernel (int8 read directly, SwiGLU fused when glu=True)."""
+        if hasattr(mod, "_fused_weight_bias"):
+            w, b = mod._fused_weight_bias()
+        else:
+            w, b = mod.weight, getattr(mod, "bias", None)
+        if not use_bias:
+            b = None
+        scale = mod._row_scale() if w.dtype == torch.int8 else None
+        M = x.numel() // x.shape[-1]
+        if w.dtype == torch.int8 or (M <= 8 and x.is_cuda):
+            return skinny_linear(x, w, scale, b, glu=glu)
+        y = _linear(x, w, b)
+        return ops.swiglu(y) if glu else y
 
     def _norm(self, x, w, residual):
         if residual is None:

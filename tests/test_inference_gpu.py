@@ -68,3 +68,20 @@ def test_graph_decode_matches_eager(hf_sd):
     s2 = e.generate(ids, max_new_tokens=20, eos_token_id=-1, do_sample=True, top_k=20, seed=3)
     assert torch.equal(s1.cpu(), s2.cpu())
     assert not torch.equal(s1[:, 40:].cpu(), a[:, 40:60].cpu())  # sampling actually samples
+
+
+def test_int8_inference_on_gpu(hf_sd):
+    cfg, sd = hf_sd
+    from neuronx_distributed_llama3_2_amd.inference import InferenceConfig, LlamaForCausalLMInference
+    from neuronx_distributed_llama3_2_amd.models.llama.convert import hf_to_nxd
+
+    icfg = InferenceConfig(batch_size=2, seq_len=256, max_context_length=128, quantized=True,
+                           quantization_type="per_channel_symmetric")
+    q = LlamaForCausalLMInference(cfg, icfg, dtype=torch.bfloat16, device=torch.device("cuda"), init_weights=False)
+    q._load_full(hf_to_nxd(sd, cfg))
+    f = _model(cfg, sd, torch.bfloat16, device=torch.device("cuda"))
+    ids = torch.randint(3, cfg.vocab_size, (2, 50))
+    a, b = f._context_encode(ids), q._context_encode(ids)
+    assert (a - b).abs().max() / a.abs().max() < 0.05
+    out = q.generate(ids, max_new_tokens=20, eos_token_id=-1)
+    assert out.shape == (2, 70)

@@ -260,3 +260,32 @@ def test_tuned_gemm_variants(M, N, K):
     exp = mg + g.float().t() @ x.float()
     gemm.wgrad_accumulate_(mg, g, x)
     torch.testing.assert_close(mg, exp, atol=1e-3 * exp.abs().max().item(), rtol=1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 3, 8])
+@pytest.mark.parametrize("wtype", ["bf16", "int8_tensor", "int8_channel"])
+@pytest.mark.parametrize("glu", [False, True])
+def test_gemv_skinny(M, wtype, glu):
+    from neuronx_distributed_llama3_2_amd.ops.gemv import dequantize_weight, skinny_linear
+    from neuronx_distributed_llama3_2_amd.quantization import quantize_symmetric
+
+    torch.manual_seed(M)
+    K, N = 2048, 1536
+    Nw = 2 * N if glu else N
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    wf = torch.randn(Nw, K, device="cuda") * 0.02
+    bias = torch.randn(Nw, device="cuda", dtype=torch.bfloat16) * 0.1
+    if wtype == "bf16":
+        w, s = wf.to(torch.bfloat16), None
+        wref = w.float()
+    else:
+        w, s = quantize_symmetric(wf, 0 if wtype == "int8_channel" else None)
+        wref = w.float() * s.reshape(-1, 1) if s.numel() > 1 else w.float() * s
+        torch.testing.assert_close(dequantize_weight(w, s).float(), wref, atol=1e-2, rtol=1e-2)
+    ref = x.float() @ wref.t() + bias.float()
+    if glu:
+        g, u = ref.chunk(2, dim=-1)
+        ref = torch.nn.functional.silu(g) * u
+    y = skinny_linear(x, w, s, bias, glu=glu)
+    assert y.shape == (M, N)
+    torch.testing.assert_close(y.float(), ref, atol=2e-2 * ref.abs().max().item(), rtol=2e-2)
