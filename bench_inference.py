@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--runs", type=int, default=10)
     ap.add_argument("--graph-steps", type=int, default=16)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--quantized", default=None, choices=[None, "per_tensor_symmetric", "per_channel_symmetric"])
     ap.add_argument("--report", default="gpurun_out/benchmark_report.json")
     args = ap.parse_args()
 
@@ -44,7 +45,9 @@ def main():
     mcfg = llama_config(args.model)
     seq_len = args.prompt + args.new
     icfg = InferenceConfig(tp_degree=world, batch_size=args.batch, seq_len=seq_len, max_context_length=args.prompt,
-                           decode_graph_steps=args.graph_steps, use_hip_graphs=not args.no_graphs)
+                           decode_graph_steps=args.graph_steps, use_hip_graphs=not args.no_graphs,
+                           quantized=args.quantized is not None,
+                           quantization_type=args.quantized or "per_tensor_symmetric")
     torch.manual_seed(0)
     model = LlamaForCausalLMInference(mcfg, icfg, dtype=torch.bfloat16)
     g = torch.Generator().manual_seed(1)
@@ -69,7 +72,8 @@ def main():
                                   "tokens_per_s_per_seq": 1000.0 * max(1, args.new - 1) / max(1e-6, e2e_ms - cte_ms)}
     report["config"] = {"model": args.model, "tp": world, "batch": args.batch, "prompt": args.prompt,
                         "new_tokens": args.new, "dtype": "bf16", "graph_steps": args.graph_steps,
-                        "hip_graphs": not args.no_graphs, "data": "synthetic prompt, random-init weights"}
+                        "hip_graphs": not args.no_graphs, "quantized": args.quantized,
+                        "data": "synthetic prompt, random-init weights"}
     if not dist.is_initialized() or dist.get_rank() == 0:
         os.makedirs(os.path.dirname(args.report) or ".", exist_ok=True)
         with open(args.report, "w") as f:

@@ -32,7 +32,7 @@ int scale_flat_launch(float*, int64_t, const float*, hipStream_t);
 int embedding_fwd_launch(const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, hipStream_t);
 int embedding_bwd_launch(const int64_t*, const void*, float*, int64_t, int, int64_t, int64_t, hipStream_t);
 int decode_attn_launch(const void*, const int64_t*, const void*, const void*, const int64_t*, const int*, const int*,
-                       float*, float*, float*, void*, const int64_t*, int, int, int, int, int, int, float, hipStream_t);
+                       float*, float*, float*, int*, void*, const int64_t*, int, int, int, int, int, int, float, hipStream_t);
 int kv_cache_write_launch(const void*, const void*, const int64_t*, void*, void*, const int64_t*, const int*, const int*,
                           int, int, int, int, int, hipStream_t);
 int argmax_launch(const void*, int, int64_t, int, int, int64_t*, hipStream_t);
@@ -343,6 +343,21 @@ void embedding_bwd(at::Tensor ids, at::Tensor dout, at::Tensor dw, int64_t start
 }
 
 // q: [B, T, Hq, D] (strided), caches: [Bc, Hkv, Lmax, D] contiguous, out: [B, T, Hq, D]
+// Zero-initialised split counters of the fused decode-attention kernel (the last workgroup of each
+// (batch, kv head) resets its counter, so the buffer stays valid across launches and graph replays).
+// Grown outside of stream capture only.
+int* decode_counters(int dev, int64_t n) {
+  static std::vector<at::Tensor> bufs;
+  if ((int)bufs.size() <= dev) bufs.resize(dev + 1);
+  if (!bufs[dev].defined() || bufs[dev].numel() < n) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(cur_stream(), &st);
+    TORCH_CHECK(st == hipStreamCaptureStatusNone, "decode_attn: first call for this batch must happen before graph capture");
+    bufs[dev] = at::zeros({std::max<int64_t>(n, 1024)}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev));
+  }
+  return bufs[dev].data_ptr<int>();
+}
+
 void decode_attn(at::Tensor q, at::Tensor kc, at::Tensor vc, c10::optional<at::Tensor> cache_idx, at::Tensor seq_len,
                  at::Tensor out, double scale, int64_t nsplit) {
   int64_t qs[3], os[3];
@@ -374,9 +389,11 @@ void decode_attn(at::Tensor q, at::Tensor kc, at::Tensor vc, c10::optional<at::T
   at::Tensor pl = at::empty({(int64_t)B * Hkv * nsplit * M}, opts);
   const int64_t cs[3] = {kc.stride(0), kc.stride(1), kc.stride(2)};
   (void)Lmax;
+  TORCH_CHECK(os[2] % 8 == 0 || Hq == 1, "out head stride must keep 16-byte alignment");
+  int* counters = decode_counters(q.device().index(), (int64_t)B * Hkv);
   check_rc(nxd::decode_attn_launch(q.data_ptr(), qs, kc.data_ptr(), vc.data_ptr(), cs, ci, seq_len.data_ptr<int>(),
-                                   po.data_ptr<float>(), pm.data_ptr<float>(), pl.data_ptr<float>(), out.data_ptr(), os, B, T,
-                                   Hq, Hkv, D, (int)nsplit, (float)scale, cur_stream()),
+                                   po.data_ptr<float>(), pm.data_ptr<float>(), pl.data_ptr<float>(), counters, out.data_ptr(),
+                                   os, B, T, Hq, Hkv, D, (int)nsplit, (float)scale, cur_stream()),
            "decode_attn");
 }
 

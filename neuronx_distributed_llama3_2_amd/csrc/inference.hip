@@ -35,14 +35,29 @@ struct DecodeParams {
   float scale;
 };
 
+// One workgroup per (batch, kv head, 128-key split); the LAST workgroup of a (batch, kv head) to
+// finish merges every split's (m, l, o) partials (agent-scope release/acquire fences around one
+// atomic counter, which that workgroup resets) — one launch per attention call, every phase fully
+// parallel over the 256 threads:
+//   scores: 2 threads per key (half the head dim each), q rows broadcast from LDS;
+//   softmax: one wave per q row over the 128 keys;
+//   P.V: thread (key group, 8-dim chunk) accumulates its keys for 8 q rows at a time, then a
+//        shuffle + LDS reduction over the key groups.
 template <int D>
-__global__ void __launch_bounds__(256) partial_kernel(DecodeParams p) {
+__global__ void __launch_bounds__(256) attn_kernel(DecodeParams p, int* __restrict__ counters, uint16_t* __restrict__ out,
+                                                   int64_t o_sb, int64_t o_st, int64_t o_sh) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NC = D / 8;          // 16-byte chunks per head row
+  constexpr int KG = 256 / NC;       // key groups in the P.V phase
+  constexpr int MB = 8;              // q rows per P.V pass
   const int G = p.Hq / p.Hkv;
   const int M = G * p.T;
-  float* qs = reinterpret_cast<float*>(smem);  // [M][D]
-  float* ss = qs + M * D;                      // [M][kChunk]
+  float* qs = reinterpret_cast<float*>(smem);   // [M][D]
+  float* ss = qs + M * D;                       // [M][kChunk]
+  float* red = ss + M * kChunk;                 // [4][MB][D]
+  __shared__ int last_flag;
 
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int split = blockIdx.x % p.nsplit;
   const int bh = blockIdx.x / p.nsplit;
   const int b = bh / p.Hkv, hkv = bh % p.Hkv;
@@ -50,110 +65,196 @@ __global__ void __launch_bounds__(256) partial_kernel(DecodeParams p) {
   const int slen = p.seq_len[b];
   const int k0 = split * kChunk;
   const int64_t pbase = ((int64_t)bh * p.nsplit + split) * M;
-
-  if (k0 >= slen) {  // nothing valid in this split
-    for (int m = threadIdx.x; m < M; m += 256) {
-      p.pm[pbase + m] = -INFINITY;
-      p.pl[pbase + m] = 0.f;
-    }
-    return;
-  }
-  // q rows m = tt * G + gg -> head hkv*G + gg, token tt
-  for (int i = threadIdx.x; i < M * (D / 8); i += 256) {
-    const int m = i / (D / 8), c = i % (D / 8);
-    const int tt = m / G, gg = m % G;
-    const uint16_t* src = p.q + (int64_t)b * p.q_sb + (int64_t)tt * p.q_st + (int64_t)(hkv * G + gg) * p.q_sh + c * 8;
-    float f[8];
-    unpack8(*reinterpret_cast<const u32x4_t*>(src), f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qs[m * D + c * 8 + j] = f[j] * p.scale;
-  }
-  __syncthreads();
   const uint16_t* kbase = p.kc + (int64_t)cb * p.c_sb + (int64_t)hkv * p.c_sh;
   const uint16_t* vbase = p.vc + (int64_t)cb * p.c_sb + (int64_t)hkv * p.c_sh;
-  {
-    const int kk = threadIdx.x & (kChunk - 1);
-    const int rp = threadIdx.x >> 7;
+
+  if (k0 < slen) {
+    // ---- q rows (pre-scaled) -> LDS
+    for (int i = tid; i < M * NC; i += 256) {
+      const int m = i / NC, c = i % NC;
+      const int tt = m / G, gg = m % G;
+      const uint16_t* src = p.q + (int64_t)b * p.q_sb + (int64_t)tt * p.q_st + (int64_t)(hkv * G + gg) * p.q_sh + c * 8;
+      float f[8];
+      unpack8(*reinterpret_cast<const u32x4_t*>(src), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qs[m * D + c * 8 + j] = f[j] * p.scale;
+    }
+    // ---- V chunk for the P.V phase: issue the loads early (independent of the scores)
+    const int c = tid % NC, kg = tid / NC;
+    constexpr int VPT = kChunk / KG;   // keys per thread
+    u32x4_t vv[VPT];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int key = k0 + kg + j * KG;
+      vv[j] = key < slen ? *reinterpret_cast<const u32x4_t*>(vbase + (int64_t)key * p.c_sl + c * 8) : u32x4_t{0, 0, 0, 0};
+    }
+    // ---- K half-row per thread
+    const int kk = tid >> 1, half = tid & 1;
     const int key = k0 + kk;
-    float kr[D];
+    float kr[D / 2];
     if (key < slen) {
 #pragma unroll
-      for (int c = 0; c < D / 8; ++c) unpack8(*reinterpret_cast<const u32x4_t*>(kbase + (int64_t)key * p.c_sl + c * 8), kr + c * 8);
+      for (int cc = 0; cc < D / 16; ++cc)
+        unpack8(*reinterpret_cast<const u32x4_t*>(kbase + (int64_t)key * p.c_sl + half * (D / 2) + cc * 8), kr + cc * 8);
+    } else {
+#pragma unroll
+      for (int d = 0; d < D / 2; ++d) kr[d] = 0.f;
     }
-    for (int m = rp; m < M; m += 2) {
+    __syncthreads();
+    for (int m = 0; m < M; ++m) {
+      const float* qr = qs + m * D + half * (D / 2);
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < D / 2; ++d) s += qr[d] * kr[d];
+      s += __shfl_xor(s, 1, 64);
       const int tt = m / G;
       const int lim = slen - (p.T - 1 - tt);  // causal among the new tokens
-      float s = -INFINITY;
-      if (key < lim) {
-        s = 0.f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) s += qs[m * D + d] * kr[d];
-      }
-      ss[m * kChunk + kk] = s;
+      if (half == 0) ss[m * kChunk + kk] = key < lim ? s : -INFINITY;
     }
-  }
-  __syncthreads();
-  {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    // ---- softmax per row (wave per row)
     for (int m = wid; m < M; m += 4) {
-      const float a = ss[m * kChunk + lane], c = ss[m * kChunk + 64 + lane];
-      const float mx = wave_max(fmaxf(a, c));
+      const float a = ss[m * kChunk + lane], e = ss[m * kChunk + 64 + lane];
+      const float mx = wave_max(fmaxf(a, e));
       const float mu = mx == -INFINITY ? 0.f : mx;
-      const float ea = __expf(a - mu), ec = __expf(c - mu);
+      const float ea = __expf(a - mu), ee = __expf(e - mu);
       ss[m * kChunk + lane] = ea;
-      ss[m * kChunk + 64 + lane] = ec;
-      const float sum = wave_sum(ea + ec);
+      ss[m * kChunk + 64 + lane] = ee;
+      const float sum = wave_sum(ea + ee);
       if (lane == 0) {
         p.pm[pbase + m] = mx;
         p.pl[pbase + m] = sum;
       }
     }
+    __syncthreads();
+    // ---- P.V
+    for (int m0 = 0; m0 < M; m0 += MB) {
+      float acc[MB][8];
+#pragma unroll
+      for (int mm = 0; mm < MB; ++mm)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[mm][j] = 0.f;
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        float vf[8];
+        unpack8(vv[j], vf);
+        const int kidx = kg + j * KG;
+#pragma unroll
+        for (int mm = 0; mm < MB; ++mm) {
+          if (m0 + mm < M) {
+            const float pv = ss[(m0 + mm) * kChunk + kidx];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[mm][e] += pv * vf[e];
+          }
+        }
+      }
+      // reduce over the key groups of this wave (lanes differing in the kg bits), then across waves
+#pragma unroll
+      for (int mm = 0; mm < MB; ++mm)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float v = acc[mm][e];
+#pragma unroll
+          for (int o = NC; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+          acc[mm][e] = v;
+        }
+      if (lane < NC) {
+#pragma unroll
+        for (int mm = 0; mm < MB; ++mm)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) red[(wid * MB + mm) * D + c * 8 + e] = acc[mm][e];
+      }
+      __syncthreads();
+      for (int i = tid; i < MB * D; i += 256) {
+        const int mm = i / D, d = i % D;
+        if (m0 + mm < M)
+          p.po[(pbase + m0 + mm) * D + d] = red[(0 * MB + mm) * D + d] + red[(1 * MB + mm) * D + d] +
+                                            red[(2 * MB + mm) * D + d] + red[(3 * MB + mm) * D + d];
+      }
+      __syncthreads();
+    }
+  } else {
+    for (int m = tid; m < M; m += 256) {
+      p.pm[pbase + m] = -INFINITY;
+      p.pl[pbase + m] = 0.f;
+    }
+  }
+  // ---- last workgroup of this (b, hkv) merges the splits
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) {
+    const int prev = atomicAdd(counters + bh, 1);
+    last_flag = prev == p.nsplit - 1;
   }
   __syncthreads();
-  const int nk = min(kChunk, slen - k0);
-  for (int i = threadIdx.x; i < M * (D / 8); i += 256) {
-    const int m = i / (D / 8), c = i % (D / 8);
+  if (!last_flag) return;
+  __threadfence();
+  const int64_t base0 = (int64_t)bh * p.nsplit * M;
+  // (1) all (split, row) maxima / sums in parallel -> LDS; per-row max and split weights
+  float* wsp = red + 4 * 8 * D;                      // [nsplit][M] split weights
+  float* rowl = ss;                                  // [M] total l per row
+  const int NSM = p.nsplit * M;
+  for (int i = tid; i < NSM; i += 256) wsp[i] = p.pm[base0 + i];
+  __syncthreads();
+  for (int m = wid; m < M; m += 4) {
+    float mx = -INFINITY;
+    for (int s2 = lane; s2 < p.nsplit; s2 += 64) mx = fmaxf(mx, wsp[s2 * M + m]);
+    mx = wave_max(mx);
+    float l = 0.f;
+    for (int s2 = lane; s2 < p.nsplit; s2 += 64) {
+      const float ms = wsp[s2 * M + m];
+      const float w = ms == -INFINITY ? 0.f : __expf(ms - mx);
+      l += w * p.pl[base0 + s2 * M + m];
+      wsp[s2 * M + m] = w;
+    }
+    l = wave_sum(l);
+    if (lane == 0) rowl[m] = l;
+  }
+  __syncthreads();
+  // (2) weighted sum of the split outputs: (row, 8-dim chunk) items x split groups, LDS reduction
+  const int items = M * NC;
+  const int SG = 256 / (items < 256 ? items : 256) > 0 ? 256 / (items < 256 ? items : 256) : 1;
+  float* part = red;                                 // [SG][items][8] (fits: SG * items <= 256)
+  for (int i0 = 0; i0 < items; i0 += 256 / SG) {
+    const int it = i0 + tid % (256 / SG), sg = tid / (256 / SG);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int kk = 0; kk < nk; ++kk) {
-      const float pv = ss[m * kChunk + kk];
-      float vf[8];
-      unpack8(*reinterpret_cast<const u32x4_t*>(vbase + (int64_t)(k0 + kk) * p.c_sl + c * 8), vf);
+    if (it < items && sg < SG) {
+      const int m = it / NC, c = it % NC;
+      for (int s2 = sg; s2 < p.nsplit; s2 += SG) {
+        const float w = wsp[s2 * M + m];
+        if (w == 0.f) continue;
+        const float* src = p.po + (base0 + (int64_t)s2 * M + m) * D + c * 8;
+        const f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(src);
+        const f32x4_t a1 = *reinterpret_cast<const f32x4_t*>(src + 4);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += pv * vf[j];
+        for (int e = 0; e < 4; ++e) {
+          acc[e] += w * a0[e];
+          acc[4 + e] += w * a1[e];
+        }
+      }
     }
-    float* dst = p.po + (pbase + m) * D + c * 8;
-    *reinterpret_cast<f32x4_t*>(dst) = f32x4_t{acc[0], acc[1], acc[2], acc[3]};
-    *reinterpret_cast<f32x4_t*>(dst + 4) = f32x4_t{acc[4], acc[5], acc[6], acc[7]};
-  }
-}
-
-// one workgroup of D threads per (b, hkv, m) row
-__global__ void combine_kernel(const float* __restrict__ po, const float* __restrict__ pm, const float* __restrict__ pl,
-                               uint16_t* __restrict__ out, int64_t o_sb, int64_t o_st, int64_t o_sh, int Hq, int Hkv,
-                               int T, int nsplit, int D) {
-  const int G = Hq / Hkv, M = G * T;
-  const int row = blockIdx.x;  // (b*Hkv + hkv)*M + m
-  const int m = row % M;
-  const int bh = row / M;
-  const int b = bh / Hkv, hkv = bh % Hkv;
-  const int tt = m / G, gg = m % G;
-  const int64_t base = (int64_t)bh * nsplit * M + m;
-  float mx = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, pm[base + (int64_t)s * M]);
-  float l = 0.f;
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float acc = 0.f;
-    l = 0.f;
-    for (int s = 0; s < nsplit; ++s) {
-      const float ms = pm[base + (int64_t)s * M];
-      if (ms == -INFINITY) continue;
-      const float wgt = __expf(ms - mx);
-      l += wgt * pl[base + (int64_t)s * M];
-      acc += wgt * po[(base + (int64_t)s * M) * D + d];
+    __syncthreads();
+    if (it < items && sg < SG) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part[(sg * (256 / SG) + (it - i0)) * 8 + e] = acc[e];
     }
-    const float o = l > 0.f ? acc / l : 0.f;
-    out[(int64_t)b * o_sb + (int64_t)tt * o_st + (int64_t)(hkv * G + gg) * o_sh + d] = f2bf(o);
+    __syncthreads();
+    if (tid < 256 / SG && i0 + tid < items) {
+      const int itm = i0 + tid, m = itm / NC, c = itm % NC;
+      float o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int g = 0; g < SG; ++g)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += part[(g * (256 / SG) + tid) * 8 + e];
+      const float inv = rowl[m] > 0.f ? 1.f / rowl[m] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] *= inv;
+      const int tt = m / G, gg = m % G;
+      *reinterpret_cast<u32x4_t*>(out + (int64_t)b * o_sb + (int64_t)tt * o_st + (int64_t)(hkv * G + gg) * o_sh + c * 8) =
+          pack8(o);
+    }
+    __syncthreads();
   }
+  if (tid == 0) counters[bh] = 0;  // ready for the next launch / graph replay
 }
 
 // cache[cb, h, pos[b] + t, :] = new[b, t, h, :]
@@ -192,9 +293,32 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const T* __restrict__ x, i
   const T* row = x + (int64_t)blockIdx.x * ld;
   float best = -INFINITY;
   int idx = 0x7fffffff;
-  for (int i = threadIdx.x; i < V; i += blockDim.x) {
-    const float v = ldv<T>(row, i);
-    if (v > best) { best = v; idx = i; }
+  if (sizeof(T) == 2 && (V % 8) == 0 && (reinterpret_cast<uintptr_t>(row) % 16) == 0) {
+    // 16-byte loads, 4 in flight per thread
+    const u32x4_t* rv = reinterpret_cast<const u32x4_t*>(row);
+    const int nv = V / 8;
+    for (int i0 = threadIdx.x; i0 < nv; i0 += 4 * blockDim.x) {
+      u32x4_t q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * blockDim.x;
+        q[u] = i < nv ? rv[i] : u32x4_t{0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u};
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float f[8];
+        unpack8(q[u], f);
+        const int base = (i0 + u * blockDim.x) * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (f[e] > best) { best = f[e]; idx = base + e; }
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < V; i += blockDim.x) {
+      const float v = ldv<T>(row, i);
+      if (v > best) { best = v; idx = i; }
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -308,7 +432,7 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(const T* __restrict__
 }  // namespace dec
 
 int decode_attn_launch(const void* q, const int64_t* qs, const void* kc, const void* vc, const int64_t* cs,
-                       const int* cache_idx, const int* seq_len, float* po, float* pm, float* pl, void* out,
+                       const int* cache_idx, const int* seq_len, float* po, float* pm, float* pl, int* counters, void* out,
                        const int64_t* os, int B, int T, int Hq, int Hkv, int D, int nsplit, float scale, hipStream_t stream) {
   using namespace dec;
   if (Hkv <= 0 || Hq % Hkv) return -1;
@@ -319,14 +443,18 @@ int decode_attn_launch(const void* q, const int64_t* qs, const void* kc, const v
   p.c_sb = cs[0]; p.c_sh = cs[1]; p.c_sl = cs[2];
   p.cache_idx = cache_idx; p.seq_len = seq_len; p.po = po; p.pm = pm; p.pl = pl;
   p.B = B; p.T = T; p.Hq = Hq; p.Hkv = Hkv; p.nsplit = nsplit; p.scale = scale;
-  const size_t lds = (size_t)M * D * 4 + (size_t)M * kChunk * 4;
+  const size_t lds = (size_t)M * D * 4 + (size_t)M * kChunk * 4 + (size_t)4 * 8 * D * 4 + (size_t)nsplit * M * 4;
   if (lds > 160 * 1024) return -3;
   const dim3 grid(B * Hkv * nsplit);
-  if (D == 64) hipLaunchKernelGGL(partial_kernel<64>, grid, dim3(256), lds, stream, p);
-  else if (D == 128) hipLaunchKernelGGL(partial_kernel<128>, grid, dim3(256), lds, stream, p);
-  else return -2;
-  hipLaunchKernelGGL(combine_kernel, dim3(B * Hkv * M), dim3(D < 256 ? D : 256), 0, stream, po, pm, pl, (uint16_t*)out,
-                     os[0], os[1], os[2], Hq, Hkv, T, nsplit, D);
+  if (D == 64) {
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)attn_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(attn_kernel<64>, grid, dim3(256), lds, stream, p, counters, (uint16_t*)out, os[0], os[1], os[2]);
+  } else if (D == 128) {
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)attn_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(attn_kernel<128>, grid, dim3(256), lds, stream, p, counters, (uint16_t*)out, os[0], os[1], os[2]);
+  } else {
+    return -2;
+  }
   return (int)hipGetLastError();
 }
 

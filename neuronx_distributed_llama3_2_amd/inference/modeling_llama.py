@@ -52,11 +52,12 @@ class LlamaInferenceModel(LlamaForCausalLM):
 
     # ------------------------------------------------------------------ KV cache
     def setup_kv_cache(self, max_batch: int, max_len: int, device=None) -> torch.Tensor:
-        device = device or self.lm_head.weight.device
+        emb = self.model.embed_tokens.weight   # activation dtype (lm_head may be int8-quantized)
+        device = device or emb.device
         L = len(self.model.layers)
         shape = (L, 2, max_batch, self.nkv, max_len, self.head_dim)
         if self.kv_cache is None or tuple(self.kv_cache.shape) != shape or self.kv_cache.device != torch.device(device):
-            self.kv_cache = torch.zeros(shape, dtype=self.lm_head.weight.dtype, device=device)
+            self.kv_cache = torch.zeros(shape, dtype=emb.dtype, device=device)
         return self.kv_cache
 
     def reset_kv_cache(self) -> None:
@@ -94,6 +95,7 @@ class LlamaInferenceModel(LlamaForCausalLM):
         cos_t, sin_t = self.model.rope_cache.tables(input_ids.device)
         pos_flat = positions.reshape(-1)
         pos0 = positions[:, 0].to(torch.int32)
+        sid32 = seq_ids.to(torch.int32) if seq_ids is not None else None   # once per step, not per layer
         emb = self.model.embed_tokens
         x = ops.vocab_parallel_embedding(input_ids, emb.weight, emb.start_index)
         x = self._all_reduce(x)
@@ -107,11 +109,11 @@ class LlamaInferenceModel(LlamaForCausalLM):
             k = qkv.view(B, T, nq + 2 * nkv, D)[:, :, nq:nq + nkv]
             v = qkv.view(B, T, nq + 2 * nkv, D)[:, :, nq + nkv:]
             kc, vc = self.kv_cache[i, 0], self.kv_cache[i, 1]
-            ops.kv_cache_write(k, v, kc, vc, pos0, seq_ids)
+            ops.kv_cache_write(k, v, kc, vc, pos0, sid32)
             if prefill:
                 o, _ = ops.flash_attn_fwd_lse(q, k, v, causal=True)
             else:
-                o = ops.decode_attention(q, kc, vc, cache_len, seq_ids)
+                o = ops.decode_attention(q, kc, vc, cache_len, sid32)
             x = self._row(attn.o_proj, o.reshape(B, T, nq * D))
             h, residual = self._norm(x, layer.post_attention_layernorm.weight, residual)
             a = self._proj(mlp.gate_up_proj, h, glu=True)   # SwiGLU fused into the decode GEMV

@@ -289,3 +289,27 @@ def test_gemv_skinny(M, wtype, glu):
     y = skinny_linear(x, w, s, bias, glu=glu)
     assert y.shape == (M, N)
     torch.testing.assert_close(y.float(), ref, atol=2e-2 * ref.abs().max().item(), rtol=2e-2)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv,T,L", [(64, 32, 8, 1, 20000), (128, 64, 8, 8, 3000), (128, 32, 8, 1, 130)])
+def test_decode_attention_long_and_repeated(D, Hq, Hkv, T, L):
+    """many splits (>64: LDS split-weight table), M = 64 rows, and back-to-back calls (counter reset)."""
+    B = 2
+    torch.manual_seed(1)
+    kc = torch.randn(B, Hkv, L, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn(B, Hkv, L, D, device=DEV, dtype=torch.bfloat16)
+    seq = torch.tensor([L - 5, L // 3], device=DEV, dtype=torch.int32)
+    kc_c, vc_c = kc.cpu(), vc.cpu()
+    for it in range(3):
+        q = torch.randn(B, T, Hq, D, device=DEV, dtype=torch.bfloat16)
+        o = ops.decode_attention(q, kc, vc, seq)
+        ro = ops.decode_attention(q.cpu(), kc_c, vc_c, seq.cpu())
+        assert _rel(o.cpu(), ro) < 2e-2, it
+
+
+def test_argmax_large_vocab():
+    x = torch.randn(3, 128256, device=DEV).to(torch.bfloat16)
+    x[1, 77777] = 50.0
+    x[2, 5] = x[2, 128255] = 60.0  # tie -> smallest index
+    a = ops.argmax_rows(x)
+    assert a.tolist() == [int(x[0].float().argmax()), 77777, 5]
