@@ -33,7 +33,95 @@ struct DecodeParams {
   float* pl;
   int B, T, Hq, Hkv, nsplit;
   float scale;
+  int fused_merge;           // 1: last workgroup merges the splits; 0: separate merge_kernel
 };
+
+// Merge the (m, l, o) partials of all splits of one (batch, kv head): every phase parallel over the
+// workgroup (split maxima/sums in LDS, (row, 8-dim chunk) x split-group partial sums, LDS reduction).
+template <int D>
+__device__ void merge_splits(const DecodeParams& p, int bh, float* red, float* ss, uint16_t* __restrict__ out,
+                             int64_t o_sb, int64_t o_st, int64_t o_sh) {
+  constexpr int NC = D / 8;
+  const int G = p.Hq / p.Hkv;
+  const int M = G * p.T;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b = bh / p.Hkv, hkv = bh % p.Hkv;
+  const int64_t base0 = (int64_t)bh * p.nsplit * M;
+  // (1) all (split, row) maxima / sums in parallel -> LDS; per-row max and split weights
+  float* wsp = red + 4 * 8 * D;                      // [nsplit][M] split weights
+  float* rowl = ss;                                  // [M] total l per row
+  const int NSM = p.nsplit * M;
+  for (int i = tid; i < NSM; i += 256) wsp[i] = p.pm[base0 + i];
+  __syncthreads();
+  for (int m = wid; m < M; m += 4) {
+    float mx = -INFINITY;
+    for (int s2 = lane; s2 < p.nsplit; s2 += 64) mx = fmaxf(mx, wsp[s2 * M + m]);
+    mx = wave_max(mx);
+    float l = 0.f;
+    for (int s2 = lane; s2 < p.nsplit; s2 += 64) {
+      const float ms = wsp[s2 * M + m];
+      const float w = ms == -INFINITY ? 0.f : __expf(ms - mx);
+      l += w * p.pl[base0 + s2 * M + m];
+      wsp[s2 * M + m] = w;
+    }
+    l = wave_sum(l);
+    if (lane == 0) rowl[m] = l;
+  }
+  __syncthreads();
+  // (2) weighted sum of the split outputs: (row, 8-dim chunk) items x split groups, LDS reduction
+  const int items = M * NC;
+  const int SG = 256 / (items < 256 ? items : 256) > 0 ? 256 / (items < 256 ? items : 256) : 1;
+  float* part = red;                                 // [SG][items][8] (fits: SG * items <= 256)
+  for (int i0 = 0; i0 < items; i0 += 256 / SG) {
+    const int it = i0 + tid % (256 / SG), sg = tid / (256 / SG);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (it < items && sg < SG) {
+      const int m = it / NC, c = it % NC;
+      for (int s2 = sg; s2 < p.nsplit; s2 += SG) {
+        const float w = wsp[s2 * M + m];
+        if (w == 0.f) continue;
+        const float* src = p.po + (base0 + (int64_t)s2 * M + m) * D + c * 8;
+        const f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(src);
+        const f32x4_t a1 = *reinterpret_cast<const f32x4_t*>(src + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[e] += w * a0[e];
+          acc[4 + e] += w * a1[e];
+        }
+      }
+    }
+    __syncthreads();
+    if (it < items && sg < SG) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part[(sg * (256 / SG) + (it - i0)) * 8 + e] = acc[e];
+    }
+    __syncthreads();
+    if (tid < 256 / SG && i0 + tid < items) {
+      const int itm = i0 + tid, m = itm / NC, c = itm % NC;
+      float o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int g = 0; g < SG; ++g)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += part[(g * (256 / SG) + tid) * 8 + e];
+      const float inv = rowl[m] > 0.f ? 1.f / rowl[m] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] *= inv;
+      const int tt = m / G, gg = m % G;
+      *reinterpret_cast<u32x4_t*>(out + (int64_t)b * o_sb + (int64_t)tt * o_st + (int64_t)(hkv * G + gg) * o_sh + c * 8) =
+          pack8(o);
+    }
+    __syncthreads();
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) merge_kernel(DecodeParams p, uint16_t* __restrict__ out, int64_t o_sb,
+                                                    int64_t o_st, int64_t o_sh) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int M = (p.Hq / p.Hkv) * p.T;
+  float* ss = reinterpret_cast<float*>(smem);   // [M] row sums
+  float* red = ss + ((M + 3) & ~3);             // [4][8][D] + [nsplit][M]
+  merge_splits<D>(p, blockIdx.x, red, ss, out, o_sb, o_st, o_sh);
+}
 
 // One workgroup per (batch, kv head, 128-key split); the LAST workgroup of a (batch, kv head) to
 // finish merges every split's (m, l, o) partials (agent-scope release/acquire fences around one
@@ -180,6 +268,7 @@ __global__ void __launch_bounds__(256) attn_kernel(DecodeParams p, int* __restri
     }
   }
   // ---- last workgroup of this (b, hkv) merges the splits
+  if (!p.fused_merge) return;
   __threadfence();
   __syncthreads();
   if (tid == 0) {
@@ -189,71 +278,7 @@ __global__ void __launch_bounds__(256) attn_kernel(DecodeParams p, int* __restri
   __syncthreads();
   if (!last_flag) return;
   __threadfence();
-  const int64_t base0 = (int64_t)bh * p.nsplit * M;
-  // (1) all (split, row) maxima / sums in parallel -> LDS; per-row max and split weights
-  float* wsp = red + 4 * 8 * D;                      // [nsplit][M] split weights
-  float* rowl = ss;                                  // [M] total l per row
-  const int NSM = p.nsplit * M;
-  for (int i = tid; i < NSM; i += 256) wsp[i] = p.pm[base0 + i];
-  __syncthreads();
-  for (int m = wid; m < M; m += 4) {
-    float mx = -INFINITY;
-    for (int s2 = lane; s2 < p.nsplit; s2 += 64) mx = fmaxf(mx, wsp[s2 * M + m]);
-    mx = wave_max(mx);
-    float l = 0.f;
-    for (int s2 = lane; s2 < p.nsplit; s2 += 64) {
-      const float ms = wsp[s2 * M + m];
-      const float w = ms == -INFINITY ? 0.f : __expf(ms - mx);
-      l += w * p.pl[base0 + s2 * M + m];
-      wsp[s2 * M + m] = w;
-    }
-    l = wave_sum(l);
-    if (lane == 0) rowl[m] = l;
-  }
-  __syncthreads();
-  // (2) weighted sum of the split outputs: (row, 8-dim chunk) items x split groups, LDS reduction
-  const int items = M * NC;
-  const int SG = 256 / (items < 256 ? items : 256) > 0 ? 256 / (items < 256 ? items : 256) : 1;
-  float* part = red;                                 // [SG][items][8] (fits: SG * items <= 256)
-  for (int i0 = 0; i0 < items; i0 += 256 / SG) {
-    const int it = i0 + tid % (256 / SG), sg = tid / (256 / SG);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (it < items && sg < SG) {
-      const int m = it / NC, c = it % NC;
-      for (int s2 = sg; s2 < p.nsplit; s2 += SG) {
-        const float w = wsp[s2 * M + m];
-        if (w == 0.f) continue;
-        const float* src = p.po + (base0 + (int64_t)s2 * M + m) * D + c * 8;
-        const f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(src);
-        const f32x4_t a1 = *reinterpret_cast<const f32x4_t*>(src + 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc[e] += w * a0[e];
-          acc[4 + e] += w * a1[e];
-        }
-      }
-    }
-    __syncthreads();
-    if (it < items && sg < SG) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) part[(sg * (256 / SG) + (it - i0)) * 8 + e] = acc[e];
-    }
-    __syncthreads();
-    if (tid < 256 / SG && i0 + tid < items) {
-      const int itm = i0 + tid, m = itm / NC, c = itm % NC;
-      float o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int g = 0; g < SG; ++g)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] += part[(g * (256 / SG) + tid) * 8 + e];
-      const float inv = rowl[m] > 0.f ? 1.f / rowl[m] : 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] *= inv;
-      const int tt = m / G, gg = m % G;
-      *reinterpret_cast<u32x4_t*>(out + (int64_t)b * o_sb + (int64_t)tt * o_st + (int64_t)(hkv * G + gg) * o_sh + c * 8) =
-          pack8(o);
-    }
-    __syncthreads();
-  }
+  merge_splits<D>(p, bh, red, ss, out, o_sb, o_st, o_sh);
   if (tid == 0) counters[bh] = 0;  // ready for the next launch / graph replay
 }
 
@@ -443,6 +468,8 @@ int decode_attn_launch(const void* q, const int64_t* qs, const void* kc, const v
   p.c_sb = cs[0]; p.c_sh = cs[1]; p.c_sl = cs[2];
   p.cache_idx = cache_idx; p.seq_len = seq_len; p.po = po; p.pm = pm; p.pl = pl;
   p.B = B; p.T = T; p.Hq = Hq; p.Hkv = Hkv; p.nsplit = nsplit; p.scale = scale;
+  static const int mode = [] { const char* e = getenv("NXD_DECODE_FUSED_MERGE"); return e ? atoi(e) : 1; }();
+  p.fused_merge = mode;
   const size_t lds = (size_t)M * D * 4 + (size_t)M * kChunk * 4 + (size_t)4 * 8 * D * 4 + (size_t)nsplit * M * 4;
   if (lds > 160 * 1024) return -3;
   const dim3 grid(B * Hkv * nsplit);
@@ -454,6 +481,16 @@ int decode_attn_launch(const void* q, const int64_t* qs, const void* kc, const v
     hipLaunchKernelGGL(attn_kernel<128>, grid, dim3(256), lds, stream, p, counters, (uint16_t*)out, os[0], os[1], os[2]);
   } else {
     return -2;
+  }
+  if (!p.fused_merge) {
+    const size_t mlds = (size_t)((M + 3) & ~3) * 4 + (size_t)4 * 8 * D * 4 + (size_t)nsplit * M * 4;
+    if (D == 64) {
+      if (mlds > 64 * 1024) (void)hipFuncSetAttribute((const void*)merge_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlds);
+      hipLaunchKernelGGL(merge_kernel<64>, dim3(B * Hkv), dim3(256), mlds, stream, p, (uint16_t*)out, os[0], os[1], os[2]);
+    } else {
+      if (mlds > 64 * 1024) (void)hipFuncSetAttribute((const void*)merge_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlds);
+      hipLaunchKernelGGL(merge_kernel<128>, dim3(B * Hkv), dim3(256), mlds, stream, p, (uint16_t*)out, os[0], os[1], os[2]);
+    }
   }
   return (int)hipGetLastError();
 }

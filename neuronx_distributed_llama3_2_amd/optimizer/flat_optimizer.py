@@ -70,16 +70,21 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
         shared = shared_param_ids or set()
         for gi, g in enumerate(self.param_groups):
             by_kind = defaultdict(list)
-            for p in g["params"]:
+            index_of = {}
+            for pi, p in enumerate(g["params"]):
                 if p.requires_grad:
                     by_kind[(param_kind(p, sp_reduce), p.dtype, p.device)].append(p)
+                    index_of[id(p)] = pi
             for (kind, _, _), plist in by_kind.items():
                 group = self.dp_group
                 if any(getattr(p, "expert_model_parallel", False) for p in plist) and ps.model_parallel_is_initialized():
                     group = ps.get_expert_data_parallel_group()
                 buf = FlatBuffer(plist, dp_group=group, zero1=zero1, shared_ids=shared, name=f"g{gi}:{kind}")
                 buf.kind = kind
-                self.buffers.append(_BufferState(buf, g))
+                st = _BufferState(buf, g)
+                st.group_index = gi
+                st.param_index = [index_of[id(p)] for p in plist]   # registration order
+                self.buffers.append(st)
 
     # ---------------------------------------------------------------- helpers
     def set_grad_sync(self, enabled: bool) -> None:
@@ -154,12 +159,17 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
         groups = [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]
         bufs = []
         for b in self.buffers:
+            layout = [(b.group_index, pi, b.buf.offsets[id(p)][0], p.numel(), tuple(p.shape))
+                      for pi, p in zip(b.param_index, b.buf.params)]
             bufs.append({"name": b.buf.name, "ranges": b.ranges, "master": b.master, "exp_avg": b.exp_avg,
-                         "exp_avg_sq": b.exp_avg_sq})
+                         "exp_avg_sq": b.exp_avg_sq, "layout": layout, "numel": b.buf.numel, "dp": b.buf.dp,
+                         "dp_rank": b.buf.dp_rank})
         return {"flat_optimizer": True, "step": self.step_count, "param_groups": groups, "buffers": bufs,
                 "zero1": self.zero1}
 
     def load_state_dict(self, sd: Dict[str, Any]) -> None:
+        if sd.get("flat_optimizer_full"):
+            return self._load_full_state_dict(sd)
         assert sd.get("flat_optimizer"), "not a FlatMixedPrecisionAdamW state dict"
         self.step_count = int(sd["step"])
         for g, sg in zip(self.param_groups, sd["param_groups"]):
@@ -171,5 +181,27 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
             b.exp_avg.copy_(sb["exp_avg"])
             b.exp_avg_sq.copy_(sb["exp_avg_sq"])
             for (s, e, lo) in b.local:
+                b.buf.param_data[s:e].copy_(b.master[lo:lo + e - s])
+            b.buf.gather_params()
+
+    def _load_full_state_dict(self, sd: Dict[str, Any]) -> None:
+        """DP-agnostic state (optimizer/convert_zero_checkpoints.py "full" format): per-parameter
+        master / exp_avg / exp_avg_sq, scattered into this rank's flat shards."""
+        self.step_count = int(sd["step"])
+        for g, sg in zip(self.param_groups, sd["param_groups"]):
+            for k, v in sg.items():
+                g[k] = v
+        states = {(int(gi), int(pi)): st for gi, pi, st in sd["param_states"]}
+        for b in self.buffers:
+            full = {k: torch.zeros(b.buf.numel, dtype=torch.float32) for k in ("master", "exp_avg", "exp_avg_sq")}
+            for pi, p in zip(b.param_index, b.buf.params):
+                st = states[(b.group_index, pi)]
+                off, n = b.buf.offsets[id(p)]
+                for k in full:
+                    full[k][off:off + n] = st[k].reshape(-1).float()
+            for (s, e, lo) in b.local:
+                b.master[lo:lo + e - s].copy_(full["master"][s:e])
+                b.exp_avg[lo:lo + e - s].copy_(full["exp_avg"][s:e])
+                b.exp_avg_sq[lo:lo + e - s].copy_(full["exp_avg_sq"][s:e])
                 b.buf.param_data[s:e].copy_(b.master[lo:lo + e - s])
             b.buf.gather_params()

@@ -49,6 +49,28 @@ def _bucket_elems() -> int:
     return int(float(os.environ.get("NXD_DP_BUCKET_MB", "128")) * 1024 * 1024 // 4)
 
 
+def plan_flat_layout(numels: Sequence[int], dp: int, cap: int, align: int = 16):
+    """Offsets of tensors (in the given order) in a flat buffer cut into buckets of ~`cap`
+    elements, each padded to a multiple of `align * dp` so every DP rank's slice stays aligned.
+    Returns (offsets, [(bucket_start, bucket_end, first_idx, end_idx)], total_numel).  Pure
+    function: the ZeRO checkpoint converter re-plans layouts for other DP sizes with it."""
+    unit = align * dp
+    offsets, spans = [], []
+    pos, bstart, first = 0, 0, 0
+    for i, n in enumerate(numels):
+        offsets.append(pos)
+        pos += (n + align - 1) // align * align
+        if pos - bstart >= cap:
+            end = (pos + unit - 1) // unit * unit
+            spans.append((bstart, end, first, i + 1))
+            pos, bstart, first = end, end, i + 1
+    if first < len(numels):
+        end = (pos + unit - 1) // unit * unit
+        spans.append((bstart, end, first, len(numels)))
+        pos = end
+    return offsets, spans, pos
+
+
 class _Bucket:
     __slots__ = ("start", "end", "params", "pending", "handle", "delayed", "out")
 
@@ -80,24 +102,11 @@ class FlatBuffer:
         pdt = self.params[0].dtype
         assert all(p.dtype == pdt and p.device == dev for p in self.params), "mixed dtype/device in one buffer"
         # ---- layout: reverse registration order (backward order), buckets of ~cap elements
-        cap = _bucket_elems()
-        unit = self.ALIGN * self.dp
-        offsets: Dict[int, Tuple[int, int]] = {}
-        buckets_spec: List[Tuple[int, int, List[torch.nn.Parameter]]] = []
-        pos, bstart, bparams = 0, 0, []
-        for p in reversed(self.params):
-            n = p.numel()
-            offsets[id(p)] = (pos, n)
-            pos += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
-            bparams.append(p)
-            if pos - bstart >= cap:
-                end = (pos + unit - 1) // unit * unit
-                buckets_spec.append((bstart, end, bparams))
-                pos, bstart, bparams = end, end, []
-        if bparams:
-            end = (pos + unit - 1) // unit * unit
-            buckets_spec.append((bstart, end, bparams))
-            pos = end
+        order = list(reversed(self.params))
+        offs, spans, total = plan_flat_layout([p.numel() for p in order], self.dp, _bucket_elems(), self.ALIGN)
+        offsets: Dict[int, Tuple[int, int]] = {id(p): (o, p.numel()) for p, o in zip(order, offs)}
+        buckets_spec = [(bs, be, order[i0:i1]) for (bs, be, i0, i1) in spans]
+        pos = total
         self.numel = pos
         self.param_data = torch.zeros(self.numel, dtype=pdt, device=dev)
         self.grad_data = torch.zeros(self.numel, dtype=grad_dtype, device=dev)

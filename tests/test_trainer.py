@@ -130,3 +130,28 @@ def test_pp2_dp2_zero1_matches_dp2():
     assert a[-1] < a[0]
     for x, y in zip(a, b):
         assert abs(x - y) < 1e-4, (a, b)
+
+
+def test_zero1_checkpoint_reshard_dp2_to_dp1():
+    """ZeRO-1 optimizer checkpoint saved at DP=2 -> convert_zero_checkpoints (full and re-sharded) ->
+    resume at DP=1 continues the DP=2 trajectory."""
+    import shutil
+
+    from neuronx_distributed_llama3_2_amd.optimizer.convert_zero_checkpoints import main as zmain
+
+    d = tempfile.mkdtemp()
+    ck = os.path.join(d, "ckpt")
+    run_distributed(_train, 2, 1, True, 6, os.path.join(d, "full.pt"), ck, False)
+    src = os.path.join(ck, "step_3")
+    full_dir = os.path.join(d, "full_tag")
+    zmain(["--input_dir", src, "--output_dir", full_dir, "--convert_to_full"])
+    assert os.path.exists(os.path.join(full_dir, "optim", "full_tp_rank_00_pp_rank_00.pt"))
+    new = os.path.join(d, "ckpt1")
+    shutil.copytree(ck, new)
+    shutil.rmtree(os.path.join(new, "step_3", "optim"))
+    zmain(["--input_dir", full_dir, "--output_dir", os.path.join(new, "step_3"), "--convert_to_sharded", "--dp_size", "1"])
+    run_distributed(_train, 1, 1, True, 6, os.path.join(d, "res.pt"), new, True)
+    full, res = torch.load(os.path.join(d, "full.pt")), torch.load(os.path.join(d, "res.pt"))
+    assert len(res) == 3
+    for x, y in zip(full[3:], res):
+        assert abs(x - y) < 1e-4, (full, res)
