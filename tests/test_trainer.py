@@ -155,3 +155,41 @@ def test_zero1_checkpoint_reshard_dp2_to_dp1():
     assert len(res) == 3
     for x, y in zip(full[3:], res):
         assert abs(x - y) < 1e-4, (full, res)
+
+
+def _dcp(rank, world, path, out):
+    import neuronx_distributed_llama3_2_amd as nxd
+    from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
+    from neuronx_distributed_llama3_2_amd.optimizer.zero_dcp_utils import load_optim_state_dict, save_optim_state_dict
+
+    cfg_nxd = nxd.neuronx_distributed_config(optimizer_config={"zero_one_enabled": True, "grad_clipping": True,
+                                                               "max_grad_norm": 1.0})
+    cfg = llama_config("tiny")
+    torch.manual_seed(0)
+    model = nxd.initialize_parallel_model(cfg_nxd, LlamaForCausalLM, cfg, torch.float32)
+    opt = nxd.initialize_parallel_optimizer(cfg_nxd, torch.optim.AdamW, model.parameters(), lr=3e-3)
+    g = torch.Generator().manual_seed(7)
+    batch = torch.randint(0, cfg.vocab_size, (4, 32), generator=g)
+    local = batch.chunk(world)[rank]
+    for _ in range(2):
+        model(local, labels=local).loss.backward()
+        opt.step()
+        opt.zero_grad()
+    inner = opt.optimizer if hasattr(opt, "optimizer") else opt
+    save_optim_state_dict(path, inner)
+    snap = [(b.master.clone(), b.exp_avg_sq.clone()) for b in inner.buffers]
+    for b in inner.buffers:
+        b.master.zero_()
+        b.exp_avg_sq.zero_()
+    load_optim_state_dict(path, inner)
+    for (m, v), b in zip(snap, inner.buffers):
+        assert torch.equal(m, b.master) and torch.equal(v, b.exp_avg_sq)
+    assert inner.step_count == 2
+    if rank == 0:
+        torch.save(True, out)
+
+
+def test_zero1_dcp_save_load():
+    d = tempfile.mkdtemp()
+    run_distributed(_dcp, 2, os.path.join(d, "dcp"), os.path.join(d, "ok.pt"))
+    assert torch.load(os.path.join(d, "ok.pt"))
