@@ -157,16 +157,6 @@ __global__ void __launch_bounds__(256) attn_kernel(DecodeParams p, int* __restri
   const uint16_t* vbase = p.vc + (int64_t)cb * p.c_sb + (int64_t)hkv * p.c_sh;
 
   if (k0 < slen) {
-    // ---- q rows (pre-scaled) -> LDS
-    for (int i = tid; i < M * NC; i += 256) {
-      const int m = i / NC, c = i % NC;
-      const int tt = m / G, gg = m % G;
-      const uint16_t* src = p.q + (int64_t)b * p.q_sb + (int64_t)tt * p.q_st + (int64_t)(hkv * G + gg) * p.q_sh + c * 8;
-      float f[8];
-      unpack8(*reinterpret_cast<const u32x4_t*>(src), f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qs[m * D + c * 8 + j] = f[j] * p.scale;
-    }
     // ---- V chunk for the P.V phase: issue the loads early (independent of the scores)
     const int c = tid % NC, kg = tid / NC;
     constexpr int VPT = kChunk / KG;   // keys per thread
@@ -187,6 +177,16 @@ __global__ void __launch_bounds__(256) attn_kernel(DecodeParams p, int* __restri
     } else {
 #pragma unroll
       for (int d = 0; d < D / 2; ++d) kr[d] = 0.f;
+    }
+    // ---- q rows (pre-scaled) -> LDS
+    for (int i = tid; i < M * NC; i += 256) {
+      const int m = i / NC, c = i % NC;
+      const int tt = m / G, gg = m % G;
+      const uint16_t* src = p.q + (int64_t)b * p.q_sb + (int64_t)tt * p.q_st + (int64_t)(hkv * G + gg) * p.q_sh + c * 8;
+      float f[8];
+      unpack8(*reinterpret_cast<const u32x4_t*>(src), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qs[m * D + c * 8 + j] = f[j] * p.scale;
     }
     __syncthreads();
     for (int m = 0; m < M; ++m) {
@@ -468,7 +468,9 @@ int decode_attn_launch(const void* q, const int64_t* qs, const void* kc, const v
   p.c_sb = cs[0]; p.c_sh = cs[1]; p.c_sl = cs[2];
   p.cache_idx = cache_idx; p.seq_len = seq_len; p.po = po; p.pm = pm; p.pl = pl;
   p.B = B; p.T = T; p.Hq = Hq; p.Hkv = Hkv; p.nsplit = nsplit; p.scale = scale;
-  static const int mode = [] { const char* e = getenv("NXD_DECODE_FUSED_MERGE"); return e ? atoi(e) : 1; }();
+  // separate merge launch by default: the fused last-workgroup merge needs agent-scope fences (L2
+  // write-back / invalidate across the 8 XCDs), measured 2-3x slower on MI355X (tools/bench_decode.py)
+  static const int mode = [] { const char* e = getenv("NXD_DECODE_FUSED_MERGE"); return e ? atoi(e) : 0; }();
   p.fused_merge = mode;
   const size_t lds = (size_t)M * D * 4 + (size_t)M * kChunk * 4 + (size_t)4 * 8 * D * 4 + (size_t)nsplit * M * 4;
   if (lds > 160 * 1024) return -3;
