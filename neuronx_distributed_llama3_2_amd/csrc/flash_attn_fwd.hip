@@ -170,28 +170,38 @@ __global__ void __launch_bounds__(kThreads, 2) fwd_kernel(FwdParams p) {
           sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, kv), qf[s], sacc[j], 0, 0, 0);
         }
       }
-      // ---- scale + mask + tile max
+      // ---- mask + tile max on the RAW scores (scale > 0 commutes with max); the scale is folded
+      // into one FMA per score below: p = exp2(s * c - m*c)
       const bool need_mask = (kt0 + kBlockN > p.Sk) || (p.causal && kt0 + kBlockN - 1 > wave_qmin);
       float tmax = -INFINITY;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          float x = sacc[j][e] * p.scale_log2;
+          float x = sacc[j][e];
           if (need_mask) {
             const int key = kt0 + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * hh;
             const bool bad = key >= p.Sk || (p.causal && key > my_q + p.causal_offset);
             x = bad ? -INFINITY : x;
+            sacc[j][e] = x;
           }
-          sacc[j][e] = x;
           tmax = fmaxf(tmax, x);
         }
       }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float m_new = fmaxf(m_i, tmax);
-      const float m_use = m_new == -INFINITY ? 0.f : m_new;
-      const float alpha = exp2f(m_i - m_use);
-      m_i = m_new;
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * p.scale_log2;
+      // deferred rescale (T13): keep the running max stale while the tile max exceeds it by less
+      // than kRescaleThreshold (log2 units); p then stays below 2^threshold, fine in fp32 / bf16,
+      // and the 4*NDB*16 accumulator multiplies are skipped on most tiles.
+      constexpr float kRescaleThreshold = 8.f;
+      if (tmax > m_i + kRescaleThreshold || m_i == -INFINITY) {
+        const float m_new = fmaxf(m_i, tmax);
+        const float alpha = (m_i == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_i - m_new);
+        m_i = m_new;
+        l_i *= alpha;
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) acc_o[db] *= alpha;
+      }
+      const float m_use = m_i == -INFINITY ? 0.f : m_i;
       float rsum = 0.f;
       bf16x8_t pf[2][2];
 #pragma unroll
@@ -200,16 +210,14 @@ __global__ void __launch_bounds__(kThreads, 2) fwd_kernel(FwdParams p) {
         for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float pv = exp2f(sacc[j][8 * s2 + e] - m_use);
+            const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j][8 * s2 + e], p.scale_log2, -m_use));
             rsum += pv;
             pf[j][s2][e] = (__bf16)pv;
           }
         }
       }
       rsum += __shfl_xor(rsum, 32, 64);
-      l_i = l_i * alpha + rsum;
-#pragma unroll
-      for (int db = 0; db < NDB; ++db) acc_o[db] *= alpha;
+      l_i += rsum;
 
       // ---- O^T += V^T P
 #pragma unroll

@@ -59,6 +59,22 @@ def bench_fa(S=8192, B=1, Hq=32, Hkv=8, D=128):
         emit(kernel="torch_sdpa_fwd_reference_only", error=str(ex)[:200])
 
 
+def bench_fa_fused_layout(S=8192, B=1, Hq=32, Hkv=8, D=128):
+    """FA on strided views of a fused [S, B, (Hq+2Hkv)*D] QKV buffer (the training model's layout)."""
+    from neuronx_distributed_llama3_2_amd.ops.flash_attn import _views
+
+    qkv = torch.randn(S, B, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    q, k, v = _views(qkv, Hq, Hkv, D)
+    flops_f = 4 * B * Hq * S * S * D / 2
+    t = timeit(lambda: ops.flash_attn_fwd_lse(q, k, v, causal=True))
+    emit(kernel="flash_fwd_fused_qkv_layout", S=S, D=D, ms=t, tflops=flops_f / t / 1e9)
+    qg, kg, vg = (x.detach().requires_grad_(True) for x in (q, k, v))
+    o = ops.flash_attn_func(qg, kg, vg, causal=True)
+    do = torch.randn_like(o)
+    t = timeit(lambda: torch.autograd.grad(o, (qg, kg, vg), do, retain_graph=True), iters=10)
+    emit(kernel="flash_bwd_fused_qkv_layout", S=S, D=D, ms=t, tflops=2.5 * flops_f / t / 1e9)
+
+
 def bench_gemm():
     dev = "cuda"
     for (M, K, N, name) in [(8192, 4096, 6144, "qkv"), (8192, 4096, 4096, "o_proj"), (8192, 4096, 28672, "gate_up"),
@@ -110,6 +126,7 @@ if __name__ == "__main__":
     torch.manual_seed(0)
     if a.only in ("all", "fa"):
         bench_fa()
+        bench_fa_fused_layout()
         bench_fa(S=4096, Hq=32, Hkv=8, D=64)
     if a.only in ("all", "gemm"):
         bench_gemm()
