@@ -56,6 +56,11 @@ def _torch_flags():
     return inc, defs, libs
 
 
+# per-TU extra flags.  flash_attn_bwd: without VGPR-form MFMAs the allocator gives the short S/dP
+# chains AGPRs and spills two of the 16 resident dK/dV accumulator tiles to scratch every tile.
+_EXTRA_FLAGS = {"flash_attn_bwd": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def _needs_build(src: Path, obj: Path, deps) -> bool:
     if not obj.exists():
         return True
@@ -84,7 +89,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         obj = BUILD_DIR / (src.stem + ".o")
         objs.append(obj)
         if force or _needs_build(src, obj, headers):
-            jobs_list.append([hipcc, *common, "-c", str(src), "-o", str(obj)])
+            jobs_list.append([hipcc, *common, *_EXTRA_FLAGS.get(src.stem, []), "-c", str(src), "-o", str(obj)])
     # host-side C++ translation units that include the torch headers (bindings, hipBLASLt tuner)
     for src in sorted(CSRC.glob("*.cpp")):
         obj = BUILD_DIR / (src.stem + ".o")

@@ -9,7 +9,8 @@
 namespace nxd {
 int flash_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, const int64_t*,
                           const int64_t*, const int64_t*, int, int, int, int, int, int, float, int, int, hipStream_t);
-int flash_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*, float*, float*,
+int64_t flash_attn_bwd_workspace(int, int, int, int, int, int);
+int flash_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*, float*,
                           void*, void*, void*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                           const int64_t*, const int64_t*, const int64_t*, const int64_t*, int, int, int, int, int, int,
                           float, int, int, hipStream_t);
@@ -114,11 +115,10 @@ void flash_attn_bwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::
   TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0, "num q heads must be a multiple of num kv heads");
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == (int64_t)B * Hq * Sq, "bad lse");
   auto opts = q.options().dtype(at::kFloat);
-  at::Tensor delta = at::empty({(int64_t)B * Hq * Sq}, opts);
-  const int64_t Sq_pad = (Sq + 31) / 32 * 32;  // bwd kernel pads query rows to its 32-row tile
-  at::Tensor dq_acc = at::empty({(int64_t)B * Hq * Sq_pad * D}, opts);
+  // fp32 workspace: dQ / dK / dV accumulators + per-row constants (sized by the kernel TU)
+  at::Tensor ws = at::empty({nxd::flash_attn_bwd_workspace(B, Sq, Sk, Hq, Hkv, D)}, opts);
   check_rc(nxd::flash_attn_bwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
-                                      lse.data_ptr<float>(), delta.data_ptr<float>(), dq_acc.data_ptr<float>(), dq.data_ptr(),
+                                      lse.data_ptr<float>(), ws.data_ptr<float>(), dq.data_ptr(),
                                       dk.data_ptr(), dv.data_ptr(), qs, ks, vs, os, dos, dqs, dks, dvs, B, Sq, Sk, Hq, Hkv, D,
                                       (float)scale, causal ? 1 : 0, (int)causal_offset, cur_stream()),
            "flash_attn_bwd");

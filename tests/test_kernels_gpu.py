@@ -88,6 +88,33 @@ def test_flash_bwd(D, causal, S):
     assert _rel(v.grad, vf.grad) < 2e-2
 
 
+def _bwd_check(B, Sq, Sk, Hq, Hkv, D, causal):
+    q, k, v = _attn_inputs(B, Sq, Sk, Hq, Hkv, D)
+    for t in (q, k, v):
+        t.requires_grad_(True)
+    o = ops.flash_attn_func(q, k, v, causal=causal)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qf, kf, vf = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ro, _ = ops.attention_reference(qf, kf, vf, causal=causal)
+    ro.backward(do.float())
+    assert _rel(q.grad, qf.grad) < 2e-2
+    assert _rel(k.grad, kf.grad) < 2e-2
+    assert _rel(v.grad, vf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_flash_bwd_chunked_items(D):
+    # one kv head (TP=8 head count): each 256-key block's query sweep is cut into several work
+    # items whose dK/dV partials meet in the fp32 atomics workspace
+    _bwd_check(1, 4096, 4096, 4, 1, D, True)
+
+
+def test_flash_bwd_cross_lengths():
+    _bwd_check(2, 100, 300, 4, 2, 64, True)  # bottom-right aligned causal, Sk not a block multiple
+    _bwd_check(1, 300, 100, 2, 2, 128, False)
+
+
 def test_rope_attention_fused_qkv():
     S, B, nq, nkv, D = 256, 2, 8, 2, 128
     W = (nq + 2 * nkv) * D

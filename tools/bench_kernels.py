@@ -33,7 +33,7 @@ def emit(**kw):
     print(json.dumps(kw), flush=True)
 
 
-def bench_fa(S=8192, B=1, Hq=32, Hkv=8, D=128):
+def bench_fa(S=8192, B=1, Hq=32, Hkv=8, D=128, sdpa=True):
     dev = "cuda"
     q = torch.randn(B, S, Hq, D, device=dev, dtype=torch.bfloat16)
     k = torch.randn(B, S, Hkv, D, device=dev, dtype=torch.bfloat16)
@@ -51,6 +51,8 @@ def bench_fa(S=8192, B=1, Hq=32, Hkv=8, D=128):
     t = timeit(bwd, iters=10)
     emit(kernel="flash_bwd", S=S, Hq=Hq, Hkv=Hkv, D=D, ms=t, tflops=2.5 * flops_f / t / 1e9)
     # vendor SDPA for context (not used by the framework)
+    if not sdpa:
+        return
     try:
         qt, kt, vt = q.transpose(1, 2), k.transpose(1, 2).repeat_interleave(Hq // Hkv, 1), v.transpose(1, 2).repeat_interleave(Hq // Hkv, 1)
         t = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(qt, kt, vt, is_causal=True))
@@ -128,6 +130,10 @@ if __name__ == "__main__":
         bench_fa()
         bench_fa_fused_layout()
         bench_fa(S=4096, Hq=32, Hkv=8, D=64)
+    if a.only in ("all", "fa", "fa_tp"):
+        # per-GPU attention shapes of Llama-3-8B under TP = 2 / 4 / 8 (heads sharded)
+        for tp in (2, 4, 8):
+            bench_fa(Hq=32 // tp, Hkv=8 // tp, sdpa=False)
     if a.only in ("all", "gemm"):
         bench_gemm()
     if a.only in ("all", "mem"):
