@@ -18,6 +18,7 @@
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPCachingAllocator.h>
 #include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>
 #include <torch/extension.h>
 
@@ -30,6 +31,7 @@
 #include <sstream>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace nxd_gemm {
@@ -59,6 +61,7 @@ struct Choice {
   size_t ws = 0;
   float ms = 0.f;
   int pos = 0;          // rank of the winner in the heuristic list (what the tune file stores)
+  int index = -1;       // exhaustive mode: the library's global solution index ("i<index>" in files)
   bool resolved = false;  // algo blob valid in this process
 };
 
@@ -107,7 +110,12 @@ class Tuner {
     cache_[key] = c;
     if (persist && !file_.empty()) {
       std::ofstream f(file_, std::ios::app);
-      if (f) f << key << " | " << c.pos << ' ' << c.ms << '\n';
+      if (f) {
+        if (c.index >= 0)
+          f << key << " | i" << c.index << ' ' << c.ms << '\n';
+        else
+          f << key << " | " << c.pos << ' ' << c.ms << '\n';
+      }
     }
   }
 
@@ -121,7 +129,13 @@ class Tuner {
  private:
   Tuner() {
     const char* m = std::getenv("NXD_GEMM_TUNE");
-    mode_ = m ? std::atoi(m) : 1;  // 0: first heuristic, 1: time the top-N heuristics
+    mode_ = m ? std::atoi(m) : 1;  // 0: first heuristic, 1: time the top-N heuristics, 2: time every solution
+    const char* t = std::getenv("NXD_GEMM_TABLE");  // read-only shipped table (tools/tune_gemm.py)
+    if (t) table_ = t;
+    const char* lk = std::getenv("NXD_GEMM_LOG_KEYS");
+    if (lk) log_ = lk;
+    const char* mx = std::getenv("NXD_GEMM_TUNE_MAX_ALGOS");
+    max_algos_ = mx ? std::max(1, std::atoi(mx)) : 4096;
     const char* c = std::getenv("NXD_GEMM_TUNE_CANDIDATES");
     candidates_ = c ? std::max(1, std::atoi(c)) : 24;
     const char* f = std::getenv("NXD_GEMM_TUNE_FILE");
@@ -131,29 +145,51 @@ class Tuner {
   }
 
   void load_file_locked() {
-    if (loaded_ || file_.empty()) {
-      loaded_ = true;
-      return;
-    }
+    if (loaded_) return;
     loaded_ = true;
-    std::ifstream f(file_);
-    std::string line;
-    while (std::getline(f, line)) {
-      auto bar = line.find('|');
-      if (bar == std::string::npos) continue;
-      std::string key = line.substr(0, bar);
-      while (!key.empty() && key.back() == ' ') key.pop_back();
-      std::istringstream s(line.substr(bar + 1));
-      Choice c;
-      if (s >> c.pos >> c.ms) cache_[key] = c;  // resolved lazily (heuristic query + pick pos)
+    for (const std::string* path : {&table_, &file_}) {  // later entries (the tune file) win
+      if (path->empty()) continue;
+      std::ifstream f(*path);
+      std::string line;
+      while (std::getline(f, line)) {
+        auto bar = line.find('|');
+        if (bar == std::string::npos) continue;
+        std::string key = line.substr(0, bar);
+        while (!key.empty() && key.back() == ' ') key.pop_back();
+        std::istringstream s(line.substr(bar + 1));
+        std::string tok;
+        Choice c;
+        if (!(s >> tok >> c.ms)) continue;
+        if (!tok.empty() && tok[0] == 'i')
+          c.index = std::atoi(tok.c_str() + 1);
+        else
+          c.pos = std::atoi(tok.c_str());
+        cache_[key] = c;  // resolved lazily (by solution index, or heuristic query + pick pos)
+      }
     }
   }
+
+ public:
+  int max_algos() const { return max_algos_; }
+
+  // NXD_GEMM_LOG_KEYS=<file>: append every problem key this process meets (once) — the input of
+  // tools/tune_gemm.py, which tunes each key offline and writes the shipped table
+  void log_key(const std::string& key) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (log_.empty() || !logged_.insert(key).second) return;
+    std::ofstream f(log_, std::ios::app);
+    if (f) f << key << '\n';
+  }
+
+ private:
 
   std::mutex mu_;
   std::vector<hipblasLtHandle_t> handles_;
   std::vector<at::Tensor> ws_;
   std::unordered_map<std::string, Choice> cache_;
-  std::string file_;
+  std::string file_, table_, log_;
+  std::unordered_set<std::string> logged_;
+  int max_algos_ = 4096;
   bool loaded_ = false;
   int mode_ = 1, candidates_ = 24;
   size_t ws_limit_ = 128u << 20;
@@ -271,7 +307,78 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
   make_descs(p, ds);
   const std::string key = p.key();
   Choice ch;
-  const bool known = T.lookup(key, &ch);
+  bool known = T.lookup(key, &ch);
+  if (!known) T.log_key(key);
+  if (known && !ch.resolved && ch.index >= 0) {
+    // a tabled global solution index: resolve it directly
+    std::vector<int> idx{ch.index};
+    std::vector<hipblasLtMatmulHeuristicResult_t> r;
+    size_t wsz = 0;
+    if (hipblaslt_ext::getAlgosFromIndex(h, idx, r) == HIPBLAS_STATUS_SUCCESS && !r.empty() &&
+        hipblaslt_ext::matmulIsAlgoSupported(h, ds.op, &alpha, ds.A, ds.B, &beta, ds.C, ds.D, r[0].algo, wsz) ==
+            HIPBLAS_STATUS_SUCCESS &&
+        wsz <= T.max_ws()) {
+      ch.algo = r[0].algo;
+      ch.ws = wsz;
+      ch.resolved = true;
+      T.store(key, ch, false);
+    } else {
+      known = false;  // stale entry (different library build): tune again
+    }
+  }
+  if (!known && T.mode() >= 2 && !capturing(s)) {
+    // exhaustive: every library solution for this (ops, dtypes), filtered by support, timed once,
+    // the five fastest re-timed
+    std::vector<hipblasLtMatmulHeuristicResult_t> all;
+    LT_CHECK(hipblaslt_ext::getAllAlgos(h, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, (hipblasOperation_t)p.opA,
+                                        (hipblasOperation_t)p.opB, (hipDataType)p.ta, (hipDataType)p.ta,
+                                        (hipDataType)p.tc, (hipDataType)p.tc, HIPBLAS_COMPUTE_32F, all));
+    const size_t wsmax = T.max_ws();
+    void* wsp = T.workspace(wsmax);
+    at::Tensor scratch;
+    void* Dp = d.data_ptr();
+    if (p.beta_nonzero) {
+      scratch = at::empty_like(d);
+      Dp = scratch.data_ptr();
+    }
+    std::vector<std::pair<float, int>> timed;
+    std::vector<size_t> wss(all.size(), 0);
+    int tried = 0;
+    for (size_t i = 0; i < all.size() && tried < T.max_algos(); ++i) {
+      size_t wsz = 0;
+      if (hipblaslt_ext::matmulIsAlgoSupported(h, ds.op, &alpha, ds.A, ds.B, &beta, ds.C, ds.D, all[i].algo, wsz) !=
+              HIPBLAS_STATUS_SUCCESS ||
+          wsz > wsmax)
+        continue;
+      ++tried;
+      wss[i] = wsz;
+      float ms = time_algo(h, ds, all[i].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(), c.data_ptr(), Dp, wsp, wsmax,
+                           s, 1);
+      if (ms > 0.f) timed.emplace_back(ms, (int)i);
+    }
+    TORCH_CHECK(!timed.empty(), "gemm: no supported hipBLASLt solution for ", key);
+    std::sort(timed.begin(), timed.end());
+    int best = timed[0].second;
+    float best_ms = 1e30f;
+    const double flops = 2.0 * M * N * K;
+    const int reps = flops > 1e12 ? 5 : (flops > 1e10 ? 10 : 30);
+    for (size_t j = 0; j < std::min<size_t>(5, timed.size()); ++j) {
+      const int i = timed[j].second;
+      float ms = time_algo(h, ds, all[i].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(), c.data_ptr(), Dp, wsp, wsmax,
+                           s, reps);
+      if (ms > 0.f && ms < best_ms) {
+        best_ms = ms;
+        best = i;
+      }
+    }
+    ch.algo = all[best].algo;
+    ch.ws = wss[best];
+    ch.ms = best_ms;
+    ch.index = hipblaslt_ext::getIndexFromAlgo(all[best].algo);
+    ch.resolved = true;
+    known = true;
+    T.store(key, ch, true);
+  }
   if (!known || !ch.resolved) {
     hipblasLtMatmulPreference_t pref;
     LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));

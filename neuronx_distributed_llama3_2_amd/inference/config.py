@@ -46,6 +46,7 @@ class InferenceConfig:
         self.quantization_type = kwargs.pop("quantization_type", "per_tensor_symmetric")
         self.trace_tokengen_model = kwargs.pop("trace_tokengen_model", True)
         self.speculation_length = kwargs.pop("speculation_length", 0)
+        self.spec_rounds_per_graph = kwargs.pop("spec_rounds_per_graph", 4)
         self.spec_batch_size = batch_size
         self.is_medusa = kwargs.pop("is_medusa", False)
         self.medusa_speculation_length = kwargs.pop("medusa_speculation_length", 0)

@@ -112,8 +112,11 @@ class LlamaForCausalLMInference:
             self._quantize()
         self.max_batch = config.max_batch_size
         self.graph_steps = max(1, int(config.decode_graph_steps))
-        # KV-cache slack so a final multi-step replay may overshoot max_length without faulting
-        self.cache_len = config.max_length + self.graph_steps
+        # KV-cache slack so a final multi-step replay (decode graph, or speculation rounds of K+1
+        # positions each) may overshoot max_length without faulting
+        K = int(getattr(config, "speculation_length", 0) or 0)
+        spec_slack = (K + 1) * int(getattr(config, "spec_rounds_per_graph", 4)) + 2 if K else 0
+        self.cache_len = config.max_length + max(self.graph_steps, spec_slack)
         self._graphs: Dict[tuple, DecodeGraph] = {}
         self._states: Dict[int, DecodeState] = {}
         self.kv_cache_populated = False
@@ -266,9 +269,27 @@ class LlamaForCausalLMInference:
     def generate(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                  max_new_tokens: Optional[int] = None, do_sample: bool = False, top_k: int = 1,
                  temperature: float = 1.0, eos_token_id=None, pad_token_id: Optional[int] = None,
-                 max_length: Optional[int] = None, seed: Optional[int] = None, **unused) -> torch.Tensor:
+                 max_length: Optional[int] = None, seed: Optional[int] = None, assistant_model=None,
+                 **unused) -> torch.Tensor:
         """HF-style generate: returns [B, T + new] token ids (right-padded prompts keep their pads,
-        tokens after EOS are `pad_token_id`)."""
+        tokens after EOS are `pad_token_id`).  `assistant_model` (another LlamaForCausalLMInference
+        with the same vocabulary) switches to greedy speculative decoding (inference/speculation.py)."""
+        if assistant_model is not None:
+            if do_sample:
+                raise ValueError("Sampling is unsupported as part of speculation. Only greedy speculation is supported.")
+            from .speculation import SpeculativeDecoder
+
+            K = int(self.config.speculation_length or 4)
+            dec = self._spec.get(id(assistant_model)) if hasattr(self, "_spec") else None
+            if dec is None:
+                dec = SpeculativeDecoder(self, assistant_model, K, int(getattr(self.config, "spec_rounds_per_graph", 4)))
+                if not hasattr(self, "_spec"):
+                    self._spec = {}
+                self._spec[id(assistant_model)] = dec
+            if max_new_tokens is None and max_length is not None:
+                max_new_tokens = max_length - input_ids.shape[1]
+            return dec.generate(input_ids, attention_mask, max_new_tokens=max_new_tokens, eos_token_id=eos_token_id,
+                                pad_token_id=pad_token_id)
         dev = self.device
         B, T = input_ids.shape
         assert B <= self.max_batch, f"batch {B} > max_batch_size {self.max_batch}"

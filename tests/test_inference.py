@@ -187,3 +187,27 @@ def test_int8_quantized_inference_close_to_float():
     q2 = LlamaForCausalLMInference.load(d, dtype=torch.float32)
     assert q2.model.model.layers[1].self_attn.o_proj.weight.dtype == torch.int8
     torch.testing.assert_close(q2._context_encode(ids), q._context_encode(ids))
+
+
+def test_speculative_decoding_matches_target_greedy():
+    """Draft + verify + accept on the device == the target's own greedy decode, whether the draft
+    agrees (same weights: K+1 tokens per round) or mostly disagrees (random draft); batched with
+    different prompt lengths (reference: utils/speculative_decoding.py _standard_assisted_decoding)."""
+    cfg = _tiny_cfg()
+    hf = _hf_model(cfg, seed=0)
+    sd = {k: v.detach().clone() for k, v in hf.state_dict().items()}
+    tgt = _inf_model(cfg, sd, max_len=64, batch=2, speculation_length=3)
+    ids = torch.randint(3, cfg.vocab_size, (2, 9))
+    mask = torch.ones_like(ids)
+    mask[1, 6:] = 0
+    ref = tgt.generate(ids, mask, max_new_tokens=20, eos_token_id=None)
+    same = _inf_model(cfg, sd, max_len=64, batch=2, speculation_length=3)
+    out = tgt.generate(ids, mask, max_new_tokens=20, eos_token_id=None, assistant_model=same)
+    assert torch.equal(out, ref)
+    dec = next(iter(tgt._spec.values()))
+    assert dec.last_stats["tokens_per_round"] > 3.5  # all K=3 drafts + the bonus token accepted
+    dcfg = _tiny_cfg(num_hidden_layers=1)
+    draft = _inf_model(dcfg, {k: v.detach().clone() for k, v in _hf_model(dcfg, seed=7).state_dict().items()},
+                       max_len=64, batch=2, speculation_length=3)
+    out2 = tgt.generate(ids, mask, max_new_tokens=20, eos_token_id=None, assistant_model=draft)
+    assert torch.equal(out2, ref)

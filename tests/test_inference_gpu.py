@@ -88,3 +88,23 @@ def test_int8_inference_on_gpu(hf_sd):
     assert (a - b).abs().max() / a.abs().max() < 0.05
     out = q.generate(ids, max_new_tokens=20, eos_token_id=-1)
     assert out.shape == (2, 70)
+
+
+def test_speculative_decoding_gpu_graphs(hf_sd):
+    """Device-resident speculation (hipGraph rounds) on MI355X: with a same-weights draft every
+    round accepts all K drafts, and the tokens follow the target's greedy decode."""
+    cfg, sd = hf_sd
+    dev = torch.device("cuda")
+    tgt = _model(cfg, sd, torch.bfloat16, device=dev)
+    tgt.config.speculation_length = 4
+    draft = _model(cfg, sd, torch.bfloat16, device=dev)
+    torch.manual_seed(5)
+    ids = torch.randint(3, cfg.vocab_size, (2, 40))
+    ref = tgt.generate(ids, max_new_tokens=48, eos_token_id=None).cpu()
+    out = tgt.generate(ids, max_new_tokens=48, eos_token_id=None, assistant_model=draft).cpu()
+    assert out.shape == ref.shape
+    dec = next(iter(tgt._spec.values()))
+    assert dec.last_stats["tokens_per_round"] > 3.0, dec.last_stats  # ~K+1 (bf16 ties may reject)
+    new_ref, new_out = ref[:, 40:], out[:, 40:]
+    assert torch.equal(new_out[:, :16], new_ref[:, :16])   # bf16: allow late divergence only
+    assert (new_out == new_ref).float().mean() > 0.9
