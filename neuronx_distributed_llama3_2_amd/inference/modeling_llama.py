@@ -83,7 +83,7 @@ class LlamaInferenceModel(LlamaForCausalLM):
     @torch.no_grad()
     def forward_tokens(self, input_ids: torch.Tensor, positions: torch.Tensor, seq_ids: Optional[torch.Tensor] = None,
                        cache_len: Optional[torch.Tensor] = None, last_index: Optional[torch.Tensor] = None,
-                       prefill: bool = False) -> torch.Tensor:
+                       prefill: bool = False, return_hidden: bool = False):
         """input_ids [B, T]; positions [B, T] (int64) absolute positions of the new tokens;
         seq_ids [B] cache rows; cache_len [B] int32 valid cache length AFTER this step (decode);
         last_index [B] -> logits [B, V] of that token per sequence, else logits [B, T, V].
@@ -123,8 +123,62 @@ class LlamaInferenceModel(LlamaForCausalLM):
             x = x[rows, last_index]
             residual = residual[rows, last_index]
         h, _ = self._norm(x, self.model.norm.weight, residual)
-        logits = self._proj(self.lm_head, h)
-        return self._gather_vocab(logits)
+        logits = self._gather_vocab(self._proj(self.lm_head, h))
+        return (logits, h) if return_hidden else logits
+
+    @torch.no_grad()
+    def forward_tree(self, tokens: torch.Tensor, positions: torch.Tensor, tree_mask: torch.Tensor, prefix_len: int,
+                     seq_id: int = 0):
+        """Medusa tree verification for ONE sequence: tokens / positions [N] (tree nodes at
+        prefix_len + depth), tree_mask [N, N] bool (node i sees node j iff j is i or an ancestor).
+        Every node also sees the cached prefix [0, prefix_len).  Nothing is written to the KV cache;
+        returns (logits [N, V], final hidden [N, H], per-layer (k, v) [N, Hkv, D] of the nodes) so
+        the caller commits only the accepted path (commit_tree_kv)."""
+        N = tokens.shape[0]
+        nq, nkv, D = self.nq, self.nkv, self.head_dim
+        g = nq // nkv
+        W = (nq + 2 * nkv) * D
+        cos_t, sin_t = self.model.rope_cache.tables(tokens.device)
+        scale = 1.0 / math.sqrt(D)
+        emb = self.model.embed_tokens
+        x = self._all_reduce(ops.vocab_parallel_embedding(tokens.view(1, N), emb.weight, emb.start_index))
+        residual = None
+        kvs = []
+        tree_bias = torch.zeros((N, N), dtype=torch.float32, device=tokens.device).masked_fill(~tree_mask, float("-inf"))
+        for i, layer in enumerate(self.model.layers):
+            attn, mlp = layer.self_attn, layer.mlp
+            h, residual = self._norm(x, layer.input_layernorm.weight, residual)
+            qkv = self._proj(attn.qkv_proj, h)
+            ops.rope_inplace_(qkv.view(N, W), 0, nq + nkv, D, cos_t, sin_t, positions.reshape(-1))
+            qkv4 = qkv.view(N, nq + 2 * nkv, D)
+            q, k, v = qkv4[:, :nq], qkv4[:, nq:nq + nkv], qkv4[:, nq + nkv:]
+            kvs.append((k.clone(), v.clone()))
+            kc = self.kv_cache[i, 0, seq_id, :, :prefix_len].float()   # [Hkv, P, D]
+            vc = self.kv_cache[i, 1, seq_id, :, :prefix_len].float()
+            qf = q.float().permute(1, 0, 2).reshape(nkv, g * N, D)    # heads grouped by kv head
+            s_c = torch.matmul(qf, kc.transpose(1, 2)) * scale         # [Hkv, g*N, P]
+            s_t = torch.matmul(qf, k.float().permute(1, 2, 0)) * scale  # [Hkv, g*N, N]
+            s_t = s_t.view(nkv, g, N, N) + tree_bias
+            s = torch.cat([s_c.view(nkv, g, N, prefix_len), s_t], -1)
+            p_ = torch.softmax(s, -1)
+            o = torch.matmul(p_[..., :prefix_len].reshape(nkv, g * N, prefix_len), vc) + \
+                torch.matmul(p_[..., prefix_len:].reshape(nkv, g * N, N), v.float().permute(1, 0, 2))
+            o = o.view(nq, N, D).permute(1, 0, 2).reshape(1, N, nq * D).to(x.dtype)
+            x = self._row(attn.o_proj, o)
+            h, residual = self._norm(x, layer.post_attention_layernorm.weight, residual)
+            x = self._row(mlp.down_proj, self._proj(mlp.gate_up_proj, h, glu=True))
+        h, _ = self._norm(x, self.model.norm.weight, residual)
+        logits = self._gather_vocab(self._proj(self.lm_head, h))
+        return logits.view(N, -1), h.view(N, -1), kvs
+
+    @torch.no_grad()
+    def commit_tree_kv(self, kvs, nodes: torch.Tensor, start: int, seq_id: int = 0) -> None:
+        """Write the K/V of the accepted tree nodes (in path order) at cache positions start..start+n."""
+        sid = torch.tensor([seq_id], dtype=torch.int32, device=nodes.device)
+        pos = torch.tensor([start], dtype=torch.int32, device=nodes.device)
+        for i, (k, v) in enumerate(kvs):
+            ops.kv_cache_write(k.index_select(0, nodes).unsqueeze(0), v.index_select(0, nodes).unsqueeze(0),
+                               self.kv_cache[i, 0], self.kv_cache[i, 1], pos, sid)
 
     def _row(self, mod, x: torch.Tensor) -> torch.Tensor:
         """Row-parallel projection: partial GEMM, TP all-reduce, then the (replicated) bias."""

@@ -21,6 +21,10 @@ def ext():
     global _C, _ERR
     if _C is not None:
         return _C
+    # shipped exhaustive hipBLASLt tuning table (tools/tune_gemm.py); NXD_GEMM_TABLE="" disables
+    table = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuned", "gemm_gfx950.txt")
+    if os.path.exists(table):
+        os.environ.setdefault("NXD_GEMM_TABLE", table)
     try:
         from .. import _C as c  # noqa: WPS433
     except ImportError as e:  # pragma: no cover - depends on the build

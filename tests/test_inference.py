@@ -211,3 +211,56 @@ def test_speculative_decoding_matches_target_greedy():
                        max_len=64, batch=2, speculation_length=3)
     out2 = tgt.generate(ids, mask, max_new_tokens=20, eos_token_id=None, assistant_model=draft)
     assert torch.equal(out2, ref)
+
+
+def test_medusa_tree_buffers_and_decoding_matches_greedy():
+    """Medusa tree verification (tree attention mask, accepted-path KV commit) reproduces the
+    target's greedy decode with arbitrary (random) Medusa heads (reference: utils/medusa_utils.py)."""
+    from neuronx_distributed_llama3_2_amd.inference.medusa import MedusaDecoder, MedusaHeads, medusa_tree_buffers
+
+    b = medusa_tree_buffers([[0], [1], [0, 0], [0, 1], [0, 0, 0]])
+    # nodes: 0 root, 1 [0], 2 [1], 3 [0,0], 4 [0,1], 5 [0,0,0]
+    assert b["position_ids"].tolist() == [0, 1, 1, 2, 2, 3]
+    assert b["attn_mask"][5].tolist() == [1, 1, 0, 1, 0, 1]
+    assert b["tree_indices"].tolist() == [0, 1, 2, 11, 12, 21]
+    paths = {tuple(r) for r in b["retrieve_indices"].tolist()}
+    assert paths == {(0, 1, 3, 5), (0, 1, 4, -1), (0, 2, -1, -1)}
+    cfg = _tiny_cfg()
+    hf = _hf_model(cfg, seed=0)
+    sd = {k: v.detach().clone() for k, v in hf.state_dict().items()}
+    tgt = _inf_model(cfg, sd, max_len=64, batch=1)
+    ids = torch.randint(3, cfg.vocab_size, (1, 7))
+    ref = tgt.generate(ids, max_new_tokens=24, eos_token_id=None)
+    torch.manual_seed(3)
+    heads = MedusaHeads(cfg.hidden_size, cfg.vocab_size, 3, dtype=torch.float32)
+    for n, p in heads.named_parameters():
+        torch.nn.init.normal_(p, std=0.05)
+    dec = MedusaDecoder(tgt, heads, [[0], [1], [0, 0], [0, 1], [0, 0, 0], [2]], topk=4)
+    out = dec.generate(ids, max_new_tokens=24)
+    assert torch.equal(out, ref), (out, ref)
+    # heads that copy the target's own lm_head one step ahead are not available here; at least
+    # every round emits >= 1 token and the tree path machinery was exercised
+    assert dec.last_stats["rounds"] <= 24
+
+
+def test_tree_attention_chain_equals_decode():
+    """forward_tree on a chain-shaped tree == multi-token decode of the same tokens."""
+    cfg = _tiny_cfg()
+    hf = _hf_model(cfg, seed=0)
+    sd = {k: v.detach().clone() for k, v in hf.state_dict().items()}
+    tgt = _inf_model(cfg, sd, max_len=64, batch=1)
+    m = tgt.model
+    ids = torch.randint(3, cfg.vocab_size, (1, 10))
+    m.forward_tokens(ids, torch.arange(10).view(1, 10), torch.zeros(1, dtype=torch.long),
+                     last_index=torch.tensor([9]), prefill=True)
+    toks = torch.randint(3, cfg.vocab_size, (4,))
+    mask = torch.tril(torch.ones(4, 4)).bool()
+    lt, _, kvs = m.forward_tree(toks, 10 + torch.arange(4), mask, 10)
+    ld = m.forward_tokens(toks.view(1, 4), (10 + torch.arange(4)).view(1, 4), torch.zeros(1, dtype=torch.long),
+                          torch.tensor([14], dtype=torch.int32))[0]
+    assert (lt - ld).abs().max() < 1e-4
+    # committing the tree K/V reproduces what the decode wrote into the cache
+    kc = m.kv_cache[:, :, 0, :, 10:14].clone()
+    m.kv_cache[:, :, 0, :, 10:14] = 0
+    m.commit_tree_kv(kvs, torch.arange(4), 10)
+    assert torch.allclose(m.kv_cache[:, :, 0, :, 10:14], kc, atol=1e-5)
