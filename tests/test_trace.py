@@ -1,0 +1,137 @@
+"""Inference trace API: parallel_model_trace (in-process TP=1 and single-controller TP=2 worker
+pool), save/load round trip, ModelBuilder with two bucketed models sharing weights, checkpoint
+sharding (reference: src/neuronx_distributed/trace/*, test/unit_test/trace)."""
+
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from neuronx_distributed_llama3_2_amd.parallel_layers import parallel_state as ps
+
+H, F = 32, 64
+
+
+class TinyMLP(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        from neuronx_distributed_llama3_2_amd.parallel_layers import ColumnParallelLinear, RowParallelLinear
+
+        self.up = ColumnParallelLinear(H, F, bias=True, gather_output=False, dtype=torch.float32)
+        self.down = RowParallelLinear(F, H, bias=True, input_is_parallel=True, dtype=torch.float32)
+
+    def forward(self, x):
+        return self.down(torch.relu(self.up(x)))
+
+
+def build_tiny():
+    return TinyMLP()
+
+
+def full_state():
+    g = torch.Generator().manual_seed(0)
+    return {"up.weight": torch.randn(F, H, generator=g) * 0.1, "up.bias": torch.randn(F, generator=g) * 0.1,
+            "down.weight": torch.randn(H, F, generator=g) * 0.1, "down.bias": torch.randn(H, generator=g) * 0.1}
+
+
+def reference(x):
+    sd = full_state()
+    return torch.relu(x @ sd["up.weight"].t() + sd["up.bias"]) @ sd["down.weight"].t() + sd["down.bias"]
+
+
+@pytest.fixture
+def clean_dist():
+    yield
+    ps.destroy_model_parallel()
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def test_trace_tp1_buckets_save_load(clean_dist):
+    from neuronx_distributed_llama3_2_amd.trace import parallel_model_load, parallel_model_save, parallel_model_trace
+
+    ex = [(torch.randn(2, H),), (torch.randn(5, H),)]
+    m = parallel_model_trace(build_tiny, ex, tp_degree=1, checkpoint_loader_callable=full_state)
+    for b in (2, 5):
+        x = torch.randn(b, H)
+        assert torch.allclose(m(x), reference(x), atol=1e-5)
+    with pytest.raises(KeyError):
+        m(torch.randn(3, H))   # no bucket for that shape
+    d = tempfile.mkdtemp()
+    parallel_model_save(m, d)
+    assert os.path.exists(os.path.join(d, "tp_00.safetensors"))
+    m2 = parallel_model_load(d)
+    x = torch.randn(5, H)
+    assert torch.allclose(m2(x), reference(x), atol=1e-5)
+
+
+def test_trace_tp2_worker_pool():
+    from neuronx_distributed_llama3_2_amd.trace import parallel_model_load, parallel_model_trace
+
+    ex = [(torch.randn(4, H),)]
+    m = parallel_model_trace(build_tiny, ex, tp_degree=2, checkpoint_loader_callable=full_state)
+    try:
+        x = torch.randn(4, H)
+        assert torch.allclose(m(x), reference(x), atol=1e-5)
+        d = tempfile.mkdtemp()
+        m.save(d)
+        assert sorted(f for f in os.listdir(d) if f.endswith(".safetensors")) == ["tp_00.safetensors",
+                                                                                   "tp_01.safetensors"]
+    finally:
+        m.close()
+    m2 = parallel_model_load(d)
+    try:
+        assert torch.allclose(m2(x), reference(x), atol=1e-5)
+    finally:
+        m2.close()
+
+
+_SHARED = {}
+
+
+def shared_module():
+    # both model instances return the SAME module (weights shared / loaded once per rank)
+    if "m" not in _SHARED:
+        _SHARED["m"] = TinyMLP()
+    return _SHARED["m"]
+
+
+def test_model_builder_two_models_shared_weights(clean_dist):
+    from neuronx_distributed_llama3_2_amd.trace import BaseModelInstance, ModelBuilder
+
+    _SHARED.clear()
+    b = ModelBuilder(router=None, tp_degree=1, checkpoint_loader=full_state)
+    b.add("context_encoding", BaseModelInstance(shared_module, None), [(torch.randn(8, H),), (torch.randn(16, H),)])
+    b.add("token_generation", BaseModelInstance(shared_module, None), [(torch.randn(1, H),)])
+    nxd = b.trace()
+    assert set(nxd.nxd_model.input_shape_map.values()) == {"context_encoding", "token_generation"}
+    for n in (1, 8, 16):
+        x = torch.randn(n, H)
+        assert torch.allclose(nxd(x), reference(x), atol=1e-5)
+    d = tempfile.mkdtemp()
+    b2 = ModelBuilder(router=None, tp_degree=2, checkpoint_loader=full_state)
+    b2.add("m", BaseModelInstance(build_tiny, None), [(torch.randn(2, H),)])
+    b2.shard_checkpoint(d)
+    from safetensors.torch import load_file
+
+    s0 = load_file(os.path.join(d, "tp0_sharded_checkpoint.safetensors"))
+    s1 = load_file(os.path.join(d, "tp1_sharded_checkpoint.safetensors"))
+    assert s0["up.weight"].shape == (F // 2, H) and s0["down.weight"].shape == (H, F // 2)
+    assert torch.equal(torch.cat([s0["up.weight"], s1["up.weight"]]), full_state()["up.weight"])
+
+
+def test_model_builder_tp2_pool():
+    from neuronx_distributed_llama3_2_amd.trace import BaseModelInstance, ModelBuilder
+
+    b = ModelBuilder(router=None, tp_degree=2, checkpoint_loader=full_state)
+    b.add("a", BaseModelInstance(build_tiny, None), [(torch.randn(3, H),)])
+    b.add("b", BaseModelInstance(build_tiny, None), [(torch.randn(6, H),)])
+    nxd = b.trace()
+    try:
+        for n in (3, 6):
+            x = torch.randn(n, H)
+            assert torch.allclose(nxd(x), reference(x), atol=1e-5)
+    finally:
+        nxd.close()
