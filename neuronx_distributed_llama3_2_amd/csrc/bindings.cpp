@@ -516,9 +516,11 @@ void dequant_int8(at::Tensor w, c10::optional<at::Tensor> scale, double tscale, 
 }  // namespace
 
 void register_gemm(pybind11::module& m);  // gemm.cpp
+void register_dataloader(pybind11::module& m);  // dataloader.cpp
 
 PYBIND11_MODULE(_C, m) {
   register_gemm(m);
+  register_dataloader(m);
   m.def("gemv", &gemv);
   m.def("dequant_int8", &dequant_int8);
   m.doc() = "CDNA4 (gfx950) kernels of neuronx_distributed_llama3_2_amd";
