@@ -1,0 +1,78 @@
+"""Example scripts run end-to-end on CPU (gloo): Llama TP+ZeRO-1 pre-training with checkpoint /
+resume and the metrics file (reference examples E1)."""
+
+import json
+import os
+import sys
+
+import torch
+
+from dist_utils import run_distributed
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _w_pretrain(rank, world, out_dir, cfg_path, steps_this_run, data):
+    sys.path.insert(0, os.path.join(ROOT, "examples", "training", "llama"))
+    import tp_zero1_llama_hf_pretrain as ex
+
+    argv = ["--model_path", cfg_path, "--tensor_parallel_size", "2", "--seq_len", "32", "--batch_size", "2",
+            "--grad_accum_usteps", "2", "--max_steps", "4", "--steps_this_run", str(steps_this_run), "--use_zero_1",
+            "--sequence_parallel_enabled", "--checkpoint_dir", os.path.join(out_dir, "ckpt"), "--checkpoint_freq",
+            "2", "--output_dir", out_dir, "--lr", "1e-3", "--warmup_steps", "1"]
+    if data:
+        argv += ["--data_dir", data]
+    loss = ex.main(argv)
+    if rank == 0:
+        torch.save(float(loss), os.path.join(out_dir, f"loss_{steps_this_run}.pt"))
+
+
+def test_llama_pretrain_example_tp2_zero1_resume(tmp_path):
+    from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import llama_config
+    from neuronx_distributed_llama3_2_amd.utils.data_loader import write_token_file
+
+    cfg = llama_config("tiny", num_hidden_layers=2, hidden_size=64, intermediate_size=128, vocab_size=256,
+                       num_attention_heads=4, num_key_value_heads=2)
+    cfg_path = str(tmp_path / "config.json")
+    with open(cfg_path, "w") as f:
+        json.dump(cfg.to_dict(), f)
+    data = str(tmp_path / "tokens.bin")
+    g = torch.Generator().manual_seed(0)
+    write_token_file(data, [torch.randint(0, 256, (20000,), generator=g).numpy()])
+    # world 4 = TP2 x DP2; 2 steps, checkpoint, then resume for the remaining 2
+    run_distributed(_w_pretrain, 4, str(tmp_path), cfg_path, 2, data)
+    assert os.path.isdir(tmp_path / "ckpt" / "step_2")
+    run_distributed(_w_pretrain, 4, str(tmp_path), cfg_path, 2, data)
+    assert os.path.isdir(tmp_path / "ckpt" / "step_4")
+    m = json.load(open(tmp_path / "results.json"))
+    names = {x["MetricName"] for x in m["results"]["metrics"]}
+    assert "Average throughput" in names and m["results"]["parameters"]["tensor_parallel_size"] == 2
+    assert torch.isfinite(torch.tensor(torch.load(tmp_path / "loss_2.pt")))
+
+
+def test_inference_runner_cli_trace_generate_check(tmp_path):
+    """examples/inference/llama3_2_runner.py on CPU: trace (shard + configs) -> load -> greedy
+    generation == HF transformers (check_accuracy) -> benchmark report."""
+    import importlib.util
+
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    cfg = LlamaConfig(hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=200, max_position_embeddings=128, tie_word_embeddings=True,
+                      eos_token_id=2, bos_token_id=1, rope_theta=500000.0)
+    torch.manual_seed(0)
+    hf_dir = str(tmp_path / "hf")
+    LlamaForCausalLM(cfg).save_pretrained(hf_dir)
+    spec = importlib.util.spec_from_file_location("runner_cli", os.path.join(ROOT, "examples", "inference",
+                                                                           "llama3_2_runner.py"))
+    cli = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(cli)
+    traced = str(tmp_path / "traced")
+    base = ["--model_path", hf_dir, "--traced_path", traced, "--max_prompt_length", "16", "--sequence_length", "40"]
+    cli.main(["trace"] + base)
+    assert os.path.exists(os.path.join(traced, "tp0_sharded_checkpoint.safetensors"))
+    out = cli.main(["generate"] + base + ["--prompt_ids", "5,6,7,8"])
+    assert out.shape == (1, 40)
+    assert cli.main(["check_accuracy"] + base + ["--prompt_ids", "5,6,7,8,9,10"]) is True
+    rep = cli.main(["benchmark"] + base + ["--num_runs", "2"])
+    assert "e2e_model" in rep and rep["e2e_model"]["latency_ms_p50"] > 0
