@@ -32,6 +32,7 @@
 #include <map>
 #include <queue>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 namespace nxd {
@@ -99,6 +100,32 @@ __device__ __forceinline__ short4_t tr_read(const char* base, int row, int col) 
 __device__ __forceinline__ int ds_off(int key, int q) { return key * 64 + (((q >> 2) ^ (key & 7)) << 3) + (q & 3) * 2; }
 
 typedef short bf16s8_t __attribute__((ext_vector_type(8)));
+
+// LDS access through a plain 32-bit byte address (the extern LDS symbol's address is folded
+// into the per-lane base registers once, so `base + constant` becomes the ds_* immediate offset
+// instead of a v_add per access).
+typedef __attribute__((address_space(3))) char lds_char_t;
+__device__ __forceinline__ uint32_t lds_addr(const char* p) { return (uint32_t)(uintptr_t)(const lds_char_t*)p; }
+template <typename T>
+__device__ __forceinline__ T lds_ld(uint32_t a) {
+  return *(const __attribute__((address_space(3))) T*)(uintptr_t)a;
+}
+template <typename T>
+__device__ __forceinline__ void lds_st(uint32_t a, const T& v) {
+  *(__attribute__((address_space(3))) T*)(uintptr_t)a = v;
+}
+__device__ __forceinline__ short4_t lds_tr(uint32_t a) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t)(uintptr_t)a);
+}
+
+// acc += A * B with the accumulator pinned to AGPRs.  The 256 resident dK/dV accumulators must
+// live in the AGPR file and every short-lived MFMA chain (S, dP, dQ) in VGPRs; hipcc's allocator
+// does not find that split by itself (it either spills two accumulator tiles every tile, or —
+// with -amdgpu-mfma-vgpr-form — puts the accumulators in VGPRs and parks addresses in AGPRs).
+template <typename TA, typename TB>
+__device__ __forceinline__ void mfma_acc_agpr(f32x16_t& acc, const TA& a, const TB& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
 
 template <int D>
 __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
@@ -186,20 +213,90 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
     }
   }
 
+  // ---- per-lane LDS byte offsets, computed ONCE (every in-loop LDS access is one of these plus a
+  // compile-time constant, so the loop spends no VALU on swizzled address math).  They hold
+  // because every image's swizzle depends only on row & 15 (key/query images) or key & 7 (dS^T),
+  // and all per-step row strides are multiples of 16 / 8.
+  const int dbq = w % NDB;                 // dQ: this wave's 32-wide d block (wave-uniform)
+  const int kr0 = (w / NDB) * KEYS_PER_DQ; // dQ: this wave's first key of the block
+  // (image bases are folded into the registers: ds_read immediates are 16-bit)
+  const uint32_t L0 = lds_addr(smem);
+  uint32_t a_q[KS], a_do[KS], a_krow[KS], a_vrow[KS];  // row reads: q/dO row r, K row 64w+r, V row 32w+r
+  uint32_t a_trq[2][NDB], a_trd[2][NDB];               // tr reads rows 4hh+tq+8j, col 32dbk+16(g&1)+4tp
+  uint32_t a_dsw[4];                       // dS^T writes: key 64w+r, q 8gq+4hh
+  uint32_t a_dsr[2], a_ktr[2];             // dQ tr reads: dS^T keys kr0+8hh+tq+4j / K rows
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int a_row = lds_off<D>(r, 2 * s + hh);
+    a_q[s] = L0 + OFF_Q + a_row;
+    a_do[s] = L0 + OFF_DO + a_row;
+    a_krow[s] = L0 + OFF_K + 64 * w * (2 * D) + a_row;
+    a_vrow[s] = L0 + OFF_V + 32 * w * (2 * D) + a_row;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int dbk = 0; dbk < NDB; ++dbk) {
+      const int col = 32 * dbk + 16 * (g & 1) + 4 * tp;
+      const int a_tr = lds_off<D>(4 * hh + tq + 8 * j, col >> 3) + (col & 7) * 2;
+      a_trq[j][dbk] = L0 + OFF_Q + a_tr;
+      a_trd[j][dbk] = L0 + OFF_DO + a_tr;
+    }
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq) a_dsw[gq] = L0 + OFF_DS + 64 * w * 64 + ds_off(r, 8 * gq + 4 * hh);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    a_dsr[j] = L0 + OFF_DS + kr0 * 64 + ds_off(8 * hh + tq + 4 * j, 16 * (g & 1) + 4 * tp);
+    const int col = 32 * dbq + 16 * (g & 1) + 4 * tp;
+    a_ktr[j] = L0 + OFF_K + kr0 * (2 * D) + lds_off<D>(8 * hh + tq + 4 * j, col >> 3) + (col & 7) * 2;
+  }
+  uint32_t a_ld = L0 + OFF_LD + 16 * hh;  // nlse / ndelta rows 8gq + 4hh
+  // opaque: otherwise the compiler re-splits each base into (lane part + big constant) and puts the
+  // v_add back into the loop (the big constants do not fit the 16-bit ds offset)
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    asm volatile("" : "+v"(a_q[s]), "+v"(a_do[s]), "+v"(a_krow[s]), "+v"(a_vrow[s]));
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+#pragma unroll
+    for (int dbk = 0; dbk < NDB; ++dbk) asm volatile("" : "+v"(a_trq[j][dbk]), "+v"(a_trd[j][dbk]));
+    asm volatile("" : "+v"(a_dsr[j]), "+v"(a_ktr[j]));
+  }
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq) asm volatile("" : "+v"(a_dsw[gq]));
+  asm volatile("" : "+v"(a_ld));
+  // per-lane global offsets of the Q / dO tile pieces this lane copies (tile-invariant)
+  int q_lane[QT_PIECES_PER_WAVE], do_lane[QT_PIECES_PER_WAVE], row_lane[QT_PIECES_PER_WAVE];
+#pragma unroll
+  for (int i = 0; i < QT_PIECES_PER_WAVE; ++i) {
+    const int piece = w * QT_PIECES_PER_WAVE + i;
+    const int row = piece * ROWS_PER_PIECE + lane / CH;
+    const int ch = swz<D>(row, lane % CH);
+    row_lane[i] = row;
+    q_lane[i] = row * (int)p.q_ss + ch * 8;
+    do_lane[i] = row * (int)p.do_ss + ch * 8;
+  }
+
   auto issue_tile = [&](int it, int buf) {
     const int hq = hkv * G + it / n_qt;
     const int qt0 = qstart + (it % n_qt) * kBlockQ;
-    const uint16_t* qb = p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
-    const uint16_t* db = p.dout + (int64_t)b * p.do_sb + (int64_t)hq * p.do_sh;
+    const uint16_t* qb = p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh + (int64_t)qt0 * p.q_ss;
+    const uint16_t* db = p.dout + (int64_t)b * p.do_sb + (int64_t)hq * p.do_sh + (int64_t)qt0 * p.do_ss;
+    const bool tail = qt0 + kBlockQ > p.Sq;  // wave-uniform
 #pragma unroll
     for (int i = 0; i < QT_PIECES_PER_WAVE; ++i) {
       const int piece = w * QT_PIECES_PER_WAVE + i;
-      const int row = piece * ROWS_PER_PIECE + lane / CH;
-      const int ch = swz<D>(row, lane % CH);
-      const int qi = min(qt0 + row, p.Sq - 1);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(qb + (int64_t)qi * p.q_ss + ch * 8),
+      int qo = q_lane[i], dof = do_lane[i];
+      if (tail) {  // clamp rows past the end of the sequence (masked later)
+        const int rr = min(row_lane[i], p.Sq - 1 - qt0);
+        const int ch = swz<D>(row_lane[i], lane % CH);
+        qo = rr * (int)p.q_ss + ch * 8;
+        dof = rr * (int)p.do_ss + ch * 8;
+      }
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(qb + qo),
                                        (__attribute__((address_space(3))) void*)(smem + OFF_Q + buf * QT_BYTES + piece * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(db + (int64_t)qi * p.do_ss + ch * 8),
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(db + dof),
                                        (__attribute__((address_space(3))) void*)(smem + OFF_DO + buf * QT_BYTES + piece * 1024), 16, 0, 0);
     }
     if (w == 0) {
@@ -222,110 +319,101 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
 
   issue_tile(it_begin, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // K image + first tile visible
+  __syncthreads();  // K / V images + first tile visible
 
-  for (int it = it_begin; it < it_end; ++it) {
-    const int buf = (it - it_begin) & 1;
+  // one tile; BUF (0/1) is a compile-time constant so every LDS offset folds into the instruction
+  auto tile = [&](auto BUFC, int it) {
+    constexpr int buf = decltype(BUFC)::value;
+    constexpr int QB = buf * QT_BYTES, DB = buf * QT_BYTES, LB = buf * 256;  // offsets from the per-lane bases
     const int hq = hkv * G + it / n_qt;
     const int qt0 = qstart + (it % n_qt) * kBlockQ;
-    // buffer buf^1 was last read in the previous iteration, closed by its final barrier
+    // buffer buf^1 was last read in the previous tile, closed by its final barrier
     if (it + 1 < it_end) issue_tile(it + 1, buf ^ 1);
-
-    // lane-derived indices re-derived from an opaque copy each iteration: otherwise the
-    // compiler hoists ~100 loop-invariant swizzled LDS addresses out of the loop and spills
-    int lane_o = lane;
-    asm volatile("" : "+v"(lane_o));
-    const int r = lane_o & 31, hh = lane_o >> 5;
-    const int tq = (lane_o & 15) >> 2, tp = lane_o & 3, g = lane_o >> 4;
-    const char* ql = smem + OFF_Q + buf * QT_BYTES;
-    const char* dl = smem + OFF_DO + buf * QT_BYTES;
-    const float* nlsel = reinterpret_cast<const float*>(smem + OFF_LD + buf * 256);
-    const float* ndell = nlsel + 32;
     const int qlast = qt0 + kBlockQ - 1 + p.causal_offset;  // last key any row of the tile may see
 
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int kc0 = wkey0 + 32 * c;
-      const int krow = 64 * w + 32 * c + r;
       if (!p.causal || kc0 <= qlast) {
         touched[c] = true;
-        // ---- S = Q K^T - LSE/scale, dP = dO V^T - delta  (key on the lane)
+        // ---- S = Q K^T - LSE/scale, dP = dO V^T - delta  (key on the lane; row constants as
+        // the initial accumulators)
         f32x16_t s_acc, dp_acc;
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
-          const int qrow = 8 * gq + 4 * hh;
-          const f32x4_t l4 = *reinterpret_cast<const f32x4_t*>(nlsel + qrow);
-          const f32x4_t d4 = *reinterpret_cast<const f32x4_t*>(ndell + qrow);
+          const f32x4_t l4 = lds_ld<f32x4_t>(a_ld + LB + 32 * gq);
+          const f32x4_t d4 = lds_ld<f32x4_t>(a_ld + LB + 128 + 32 * gq);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             s_acc[4 * gq + i] = l4[i];
             dp_acc[4 * gq + i] = d4[i];
           }
         }
-        // operands one step ahead (register pressure: 256 accumulators are resident; the TU is
-        // built with -amdgpu-mfma-vgpr-form so these short MFMA chains stay in VGPRs and the
-        // AGPR file holds exactly the dK/dV accumulators — see _build.py)
-        u32x4_t qa_n = *reinterpret_cast<const u32x4_t*>(ql + lds_off<D>(r, hh));
-        u32x4_t kk_n = *reinterpret_cast<const u32x4_t*>(smem + OFF_K + lds_off<D>(krow, hh));
-        u32x4_t da_n = *reinterpret_cast<const u32x4_t*>(dl + lds_off<D>(r, hh));
-        u32x4_t vv_n = {0, 0, 0, 0};
-        if (c == 1) vv_n = *reinterpret_cast<const u32x4_t*>(smem + OFF_V + lds_off<D>(32 * w + r, hh));
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-          const u32x4_t qa = qa_n, kk = kk_n, da = da_n, vv = vv_n;
-          if (s + 1 < KS) {
-            qa_n = *reinterpret_cast<const u32x4_t*>(ql + lds_off<D>(r, 2 * s + 2 + hh));
-            kk_n = *reinterpret_cast<const u32x4_t*>(smem + OFF_K + lds_off<D>(krow, 2 * s + 2 + hh));
-            da_n = *reinterpret_cast<const u32x4_t*>(dl + lds_off<D>(r, 2 * s + 2 + hh));
-            if (c == 1) vv_n = *reinterpret_cast<const u32x4_t*>(smem + OFF_V + lds_off<D>(32 * w + r, 2 * s + 2 + hh));
-          }
+          const u32x4_t qa = lds_ld<u32x4_t>(a_q[s] + QB);
+          const u32x4_t kk = lds_ld<u32x4_t>(a_krow[s] + c * 32 * (2 * D));
+          const u32x4_t da = lds_ld<u32x4_t>(a_do[s] + DB);
           s_acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, qa), __builtin_bit_cast(bf16x8_t, kk), s_acc, 0, 0, 0);
-          dp_acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, da), c == 0 ? vf[s] : __builtin_bit_cast(bf16x8_t, vv), dp_acc, 0, 0, 0);
+          bf16x8_t vb;
+          if (c == 0) {
+            vb = vf[s];
+          } else {
+            vb = __builtin_bit_cast(bf16x8_t, lds_ld<u32x4_t>(a_vrow[s]));
+          }
+          dp_acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, da), vb, dp_acc, 0, 0, 0);
         }
         // ---- P, dS (element e of the lane: query row 8(e>>2) + 4hh + (e&3), key kc0 + r)
-        const int my_key = kc0 + r;
         const bool need_mask = (p.causal && kc0 + 31 > qt0 + p.causal_offset) || qt0 + kBlockQ > p.Sq || kc0 + 32 > p.Sk;
         bf16x8_t pf[2], dsf[2];
+        if (!need_mask) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          float pv = __builtin_amdgcn_exp2f(s_acc[e] * p.scale_log2);
-          if (need_mask) {
+          for (int e = 0; e < 16; ++e) {
+            const float pv = __builtin_amdgcn_exp2f(s_acc[e] * p.scale_log2);
+            pf[e >> 3][e & 7] = (__bf16)pv;
+            dsf[e >> 3][e & 7] = (__bf16)(pv * dp_acc[e]);
+          }
+        } else {
+          const int my_key = kc0 + r;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            float pv = __builtin_amdgcn_exp2f(s_acc[e] * p.scale_log2);
             const int qg = qt0 + 8 * (e >> 2) + 4 * hh + (e & 3);
             const bool bad = qg >= p.Sq || my_key >= p.Sk || (p.causal && my_key > qg + p.causal_offset);
             pv = bad ? 0.f : pv;
+            pf[e >> 3][e & 7] = (__bf16)pv;
+            dsf[e >> 3][e & 7] = (__bf16)(pv * dp_acc[e]);
           }
-          pf[e >> 3][e & 7] = (__bf16)pv;
-          dsf[e >> 3][e & 7] = (__bf16)(pv * dp_acc[e]);
         }
         // ---- dS -> LDS (transposed image [key][q]); whole-vector bit casts (per-element
         // extraction of bf16 ext_vectors miscompiles on ROCm 7.2)
         const u32x4_t ds_w0 = __builtin_bit_cast(u32x4_t, dsf[0]);
         const u32x4_t ds_w1 = __builtin_bit_cast(u32x4_t, dsf[1]);
-        *reinterpret_cast<u32x2_t*>(smem + OFF_DS + ds_off(krow, 0 + 4 * hh)) = u32x2_t{ds_w0[0], ds_w0[1]};
-        *reinterpret_cast<u32x2_t*>(smem + OFF_DS + ds_off(krow, 8 + 4 * hh)) = u32x2_t{ds_w0[2], ds_w0[3]};
-        *reinterpret_cast<u32x2_t*>(smem + OFF_DS + ds_off(krow, 16 + 4 * hh)) = u32x2_t{ds_w1[0], ds_w1[1]};
-        *reinterpret_cast<u32x2_t*>(smem + OFF_DS + ds_off(krow, 24 + 4 * hh)) = u32x2_t{ds_w1[2], ds_w1[3]};
+        lds_st(a_dsw[0] + c * 32 * 64, u32x2_t{ds_w0[0], ds_w0[1]});
+        lds_st(a_dsw[1] + c * 32 * 64, u32x2_t{ds_w0[2], ds_w0[3]});
+        lds_st(a_dsw[2] + c * 32 * 64, u32x2_t{ds_w1[0], ds_w1[1]});
+        lds_st(a_dsw[3] + c * 32 * 64, u32x2_t{ds_w1[2], ds_w1[3]});
         // ---- dV += P^T dO ; dK += dS^T Q   (B operands by transposed reads of the tile images)
+        if (!(p.ablate & 8)) {
 #pragma unroll
-        for (int s2 = 0; s2 < ((p.ablate & 8) ? 0 : 2); ++s2) {
-          const int R0 = 16 * s2 + 4 * hh;
+          for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
-          for (int dbk = 0; dbk < NDB; ++dbk) {
-            const int col = 32 * dbk + 16 * (g & 1) + 4 * tp;
-            const short4_t dlo = tr_read<D>(dl, R0 + tq, col);
-            const short4_t dhi = tr_read<D>(dl, R0 + 8 + tq, col);
-            const bf16s8_t db8 = {dlo[0], dlo[1], dlo[2], dlo[3], dhi[0], dhi[1], dhi[2], dhi[3]};
-            acc_dv[c][dbk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[s2], __builtin_bit_cast(bf16x8_t, db8), acc_dv[c][dbk], 0, 0, 0);
-            const short4_t qlo = tr_read<D>(ql, R0 + tq, col);
-            const short4_t qhi = tr_read<D>(ql, R0 + 8 + tq, col);
-            const bf16s8_t qb8 = {qlo[0], qlo[1], qlo[2], qlo[3], qhi[0], qhi[1], qhi[2], qhi[3]};
-            acc_dk[c][dbk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dsf[s2], __builtin_bit_cast(bf16x8_t, qb8), acc_dk[c][dbk], 0, 0, 0);
+            for (int dbk = 0; dbk < NDB; ++dbk) {
+              const int o = s2 * 16 * (2 * D);
+              const short4_t dlo = lds_tr(a_trd[0][dbk] + DB + o);
+              const short4_t dhi = lds_tr(a_trd[1][dbk] + DB + o);
+              const bf16s8_t db8 = {dlo[0], dlo[1], dlo[2], dlo[3], dhi[0], dhi[1], dhi[2], dhi[3]};
+              mfma_acc_agpr(acc_dv[c][dbk], pf[s2], db8);
+              const short4_t qlo = lds_tr(a_trq[0][dbk] + QB + o);
+              const short4_t qhi = lds_tr(a_trq[1][dbk] + QB + o);
+              const bf16s8_t qb8 = {qlo[0], qlo[1], qlo[2], qlo[3], qhi[0], qhi[1], qhi[2], qhi[3]};
+              mfma_acc_agpr(acc_dk[c][dbk], dsf[s2], qb8);
+            }
           }
         }
       } else {
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq)
-          *reinterpret_cast<u32x2_t*>(smem + OFF_DS + ds_off(krow, 8 * gq + 4 * hh)) = u32x2_t{0, 0};
+        for (int gq = 0; gq < 4; ++gq) lds_st(a_dsw[gq] + c * 32 * 64, u32x2_t{0, 0});
       }
     }
     // dS^T complete.  Raw barrier: the tile prefetch (LDS-DMA) stays in flight across it.
@@ -333,10 +421,7 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
     __builtin_amdgcn_s_barrier();
 
     // ---- dQ[q][d] += dS[q][key] K[key][d] over this wave's (d block, key range)
-    const int dbk = w % NDB;
-    const int kr0 = (w / NDB) * KEYS_PER_DQ;
-    // key groups of 16 that hold any unmasked key
-    int nks = KEYS_PER_DQ / 16;
+    int nks = KEYS_PER_DQ / 16;  // key groups of 16 that hold any unmasked key
     if (p.causal) nks = max(0, min(nks, (qlast - (kb0 + kr0) + 16) / 16));
     if (p.ablate & 4) nks = 0;
     // two independent accumulation chains (even / odd key groups): a single chain of dependent
@@ -345,14 +430,11 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
 #pragma unroll
     for (int s = 0; s < KEYS_PER_DQ / 16; ++s) {
       if (s < nks) {
-        const int kr = kr0 + 16 * s + 8 * hh;  // first key of this lane-half's 8
-        const int qc = 16 * (g & 1) + 4 * tp;
-        const short4_t a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t)(smem + OFF_DS + ds_off(kr + tq, qc)));
-        const short4_t a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t)(smem + OFF_DS + ds_off(kr + 4 + tq, qc)));
+        const short4_t a0 = lds_tr(a_dsr[0] + s * 16 * 64);
+        const short4_t a1 = lds_tr(a_dsr[1] + s * 16 * 64);
         const bf16s8_t a8 = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-        const int col = 32 * dbk + 16 * (g & 1) + 4 * tp;
-        const short4_t b0 = tr_read<D>(smem + OFF_K, kr + tq, col);
-        const short4_t b1 = tr_read<D>(smem + OFF_K, kr + 4 + tq, col);
+        const short4_t b0 = lds_tr(a_ktr[0] + s * 16 * (2 * D));
+        const short4_t b1 = lds_tr(a_ktr[1] + s * 16 * (2 * D));
         const bf16s8_t b8 = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
         if (s & 1)
           acc_dq2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a8), __builtin_bit_cast(bf16x8_t, b8), acc_dq2, 0, 0, 0);
@@ -364,7 +446,7 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
     bool adder = nks > 0 && !(p.ablate & 1);
     if constexpr (KEY_SPLIT == 2) {
       // key-half 1 hands its partial to key-half 0 through LDS (no doubled atomics)
-      float* red = reinterpret_cast<float*>(smem + OFF_RED) + (dbk * 64 + lane) * 16;
+      float* red = reinterpret_cast<float*>(smem + OFF_RED) + (dbq * 64 + lane) * 16;
       if (w >= NDB) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -386,20 +468,25 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
     if (adder) {
       // 16 UNCONDITIONAL atomics per lane (dq_acc has Sq padded to kBlockQ rows), so the
       // counted wait below knows exactly how many of this wave's VM ops are atomics.
-      float* dqb = p.dq_acc + (((int64_t)b * p.Hq + hq) * Sq_pad) * D + 32 * dbk + r;
+      float* dqb = p.dq_acc + (((int64_t)b * p.Hq + hq) * Sq_pad + qt0 + 4 * hh) * D + 32 * dbq + r;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int qg = qt0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-        atomicAdd(dqb + (int64_t)qg * D, acc_dq[e]);
-      }
+      for (int e = 0; e < 16; ++e) atomicAdd(dqb + ((e & 3) + 8 * (e >> 2)) * D, acc_dq[e]);
       // retire the tile prefetch (issued before the atomics) but leave the 16 atomics in flight
       asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();  // dS^T / Q / dO reads done; next tile landed for every wave
+  };
+
+  for (int it = it_begin; it < it_end; it += 2) {
+    tile(std::integral_constant<int, 0>{}, it);
+    if (it + 1 < it_end) tile(std::integral_constant<int, 1>{}, it + 1);
   }
 
+  // the dK/dV MFMAs are inline asm (invisible to the hazard recognizer): give the last ones their
+  // pass latency before the accumulators are read
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   // ---- dK, dV partials -> fp32 workspace: C rows = key, col = d (d on the lane)
 #pragma unroll
   for (int c = 0; c < 2; ++c) {

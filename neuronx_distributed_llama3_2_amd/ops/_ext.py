@@ -21,10 +21,9 @@ def ext():
     global _C, _ERR
     if _C is not None:
         return _C
-    # shipped exhaustive hipBLASLt tuning table (tools/tune_gemm.py); NXD_GEMM_TABLE="" disables
-    table = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuned", "gemm_gfx950.txt")
-    if os.path.exists(table):
-        os.environ.setdefault("NXD_GEMM_TABLE", table)
+    # The shipped exhaustive hipBLASLt table (tuned/gemm_gfx950.txt, tools/tune_gemm.py) is opt-in
+    # (NXD_GEMM_TABLE=<path>): measured in the full 1-GPU bench, the in-process top-24 tuning of
+    # the first step picks faster solutions (16.8k vs 16.3k tokens/s, profiles/r1_gemm_table_ab.txt).
     try:
         from .. import _C as c  # noqa: WPS433
     except ImportError as e:  # pragma: no cover - depends on the build
