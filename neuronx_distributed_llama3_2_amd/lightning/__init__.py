@@ -1,0 +1,28 @@
+"""PyTorch-Lightning integration (reference: src/neuronx_distributed/lightning/*).
+
+MI355X mapping: the XLA strategy / accelerator / launcher become a strategy over one process per
+GPU (torchrun or Lightning's own subprocess launcher) that initialises the NxD process-group mesh
+(TP/PP/EP/DP over RCCL), hands out DP-rank data shards, leaves DP gradient reduction to the
+framework's flat-buffer optimizer (no DDP wrapper), and checkpoints through the NxD sharded
+checkpoint API.  Lightning is an optional dependency: `lightning` (2.x) or `pytorch_lightning`
+must be importable; it is NOT installed in this build environment, so these classes are written
+against its public API and import-gated (parity unpinned by tests here).
+"""
+
+from ._compat import HAVE_LIGHTNING, require_lightning  # noqa: F401
+
+_EXPORTS = {
+    "NeuronXLAStrategy": ".strategy", "NxDStrategy": ".strategy",
+    "NeuronXLAAccelerator": ".accelerator", "NeuronCheckpointIO": ".checkpoint_io",
+    "NeuronLTModule": ".module", "NeuronXLAPrecisionPlugin": ".precision_plugin",
+    "NeuronTQDMProgressBar": ".progress_bar", "NeuronTensorBoardLogger": ".logger",
+}
+
+
+def __getattr__(name):
+    if name in _EXPORTS:
+        require_lightning()
+        import importlib
+
+        return getattr(importlib.import_module(_EXPORTS[name], __name__), name)
+    raise AttributeError(name)
