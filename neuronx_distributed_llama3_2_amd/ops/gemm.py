@@ -50,9 +50,31 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> torch.
     return y
 
 
+_WGRAD_BF16 = os.environ.get("NXD_WGRAD_BF16", "0") == "1"
+_scratch = {}
+
+
+def _wgrad_scratch(n: int, dtype, device) -> torch.Tensor:
+    key = (dtype, str(device))
+    t = _scratch.get(key)
+    if t is None or t.numel() < n:
+        t = _scratch[key] = torch.empty(n, dtype=dtype, device=device)
+    return t[:n]
+
+
 def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor) -> None:
-    """mg [N, K] (fp32) += go2[T, N]^T @ x2[T, K]."""
+    """mg [N, K] (fp32) += go2[T, N]^T @ x2[T, K].
+
+    Default: one hipBLASLt GEMM with fp32 C/D and beta = 1.  NXD_WGRAD_BF16=1: bf16-output GEMM
+    into a reused scratch, then an fp32 add (the per-micro-batch weight gradient is rounded to
+    bf16 before the fp32 accumulation — the precision of the reference's XLA matmul + fp32
+    grad accumulation; hipBLASLt's bf16-output solutions run faster than its fp32-output ones)."""
     if _native(go2, x2) and mg.is_contiguous():
+        if _WGRAD_BF16:
+            tmp = _wgrad_scratch(mg.numel(), go2.dtype, go2.device).view(mg.shape)
+            ext().gemm(go2.t(), x2, tmp, None, 1.0, 0.0)
+            mg.add_(tmp)
+            return
         ext().gemm(go2.t(), x2, mg, None, 1.0, 1.0)
         return
     if go2.is_cuda:
