@@ -63,7 +63,8 @@ struct BwdParams {
   int causal_offset;
   int chunk;   // max (q head, q tile) iterations per work item
   int ablate;  // timing-only ablations (NXD_FAB_ABLATE; outputs wrong): 1 no dQ atomics,
-               // 2 no dK/dV atomics, 4 no dQ MFMAs, 8 no dV/dK MFMAs
+               // 2 no dK/dV atomics, 4 no dQ MFMAs, 8 no dV/dK MFMAs, 16 no Q/dO tile loads,
+               // 32 no per-tile barriers
 };
 
 // (q head x q tile) iterations of key block kb
@@ -122,9 +123,13 @@ __device__ __forceinline__ short4_t lds_tr(uint32_t a) {
 // live in the AGPR file and every short-lived MFMA chain (S, dP, dQ) in VGPRs; hipcc's allocator
 // does not find that split by itself (it either spills two accumulator tiles every tile, or —
 // with -amdgpu-mfma-vgpr-form — puts the accumulators in VGPRs and parks addresses in AGPRs).
+// The asm is invisible to the hazard recognizer, so it carries the one wait it needs itself: a
+// VALU write of a VGPR read as SrcA/SrcB by an MFMA needs 2 wait states (hipcc emits the same
+// `s_nop 1` for the builtin form); SrcC/vDst are AGPRs no VALU touches inside the loop, and the
+// epilogue waits out the last MFMAs before reading them.
 template <typename TA, typename TB>
 __device__ __forceinline__ void mfma_acc_agpr(f32x16_t& acc, const TA& a, const TB& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
 template <int D>
@@ -328,7 +333,7 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
     const int hq = hkv * G + it / n_qt;
     const int qt0 = qstart + (it % n_qt) * kBlockQ;
     // buffer buf^1 was last read in the previous tile, closed by its final barrier
-    if (it + 1 < it_end) issue_tile(it + 1, buf ^ 1);
+    if (it + 1 < it_end && !(p.ablate & 16)) issue_tile(it + 1, buf ^ 1);
     const int qlast = qt0 + kBlockQ - 1 + p.causal_offset;  // last key any row of the tile may see
 
 #pragma unroll
@@ -418,7 +423,7 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
     }
     // dS^T complete.  Raw barrier: the tile prefetch (LDS-DMA) stays in flight across it.
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!(p.ablate & 32)) __builtin_amdgcn_s_barrier();
 
     // ---- dQ[q][d] += dS[q][key] K[key][d] over this wave's (d block, key range)
     int nks = KEYS_PER_DQ / 16;  // key groups of 16 that hold any unmasked key
@@ -476,7 +481,7 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
     } else {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
-    __builtin_amdgcn_s_barrier();  // dS^T / Q / dO reads done; next tile landed for every wave
+    if (!(p.ablate & 32)) __builtin_amdgcn_s_barrier();  // dS^T / Q / dO reads done; next tile landed
   };
 
   for (int it = it_begin; it < it_end; it += 2) {
