@@ -28,3 +28,17 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _no_leaked_process_group():
+    """Tests that initialise torch.distributed in the pytest process itself (TP=1 in-process
+    paths) must not leak the group into the next test of the same (xdist) worker."""
+    yield
+    import torch.distributed as dist
+
+    from neuronx_distributed_llama3_2_amd.parallel_layers import parallel_state as ps
+
+    ps.destroy_model_parallel()
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
