@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from neuronx_distributed_llama3_2_amd.inference.runner import LlamaRunner  # noqa: E402
 
 
-def main(argv=None):
+def main(argv=None, runner_cls=LlamaRunner):
     p = argparse.ArgumentParser()
     p.add_argument("mode", choices=["trace", "generate", "check_accuracy", "benchmark"])
     p.add_argument("--model_path", default=None)
@@ -38,7 +38,7 @@ def main(argv=None):
     p.add_argument("--do_sample", action="store_true")
     p.add_argument("--num_runs", type=int, default=20)
     a = p.parse_args(argv)
-    r = LlamaRunner(model_path=a.model_path, tokenizer_path=a.tokenizer_path or a.model_path)
+    r = runner_cls(model_path=a.model_path, tokenizer_path=a.tokenizer_path or a.model_path)
     if a.mode == "trace":
         r.trace(a.traced_path, tp_degree=a.tp_degree, batch_size=a.batch_size, max_prompt_length=a.max_prompt_length,
                 sequence_length=a.sequence_length, quantized=a.quantized, quantization_type=a.quantization_type,

@@ -42,6 +42,8 @@ int topk_sample_launch(const void*, int, int64_t, int, int, int, float, const fl
 int gemv_launch(const void*, int64_t, const void*, int64_t, int, const float*, float, const void*, void*, int64_t, int, int,
                 int, int, hipStream_t);
 int dequant_int8_launch(const void*, int64_t, const float*, float, void*, int, int, hipStream_t);
+int expert_gemv_launch(const void*, int64_t, const void*, int64_t, int64_t, const int32_t*, int, int, void*, int64_t, int,
+                       int, int, hipStream_t);
 }  // namespace nxd
 
 namespace {
@@ -497,6 +499,30 @@ void gemv(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> scale, double ts
            "gemv");
 }
 
+// x [X, K] bf16, w [E, Nw, K] bf16 (unit inner stride), eidx [P] int32 (values < E), y [P, N]
+void expert_gemv(at::Tensor x, at::Tensor w, at::Tensor eidx, int64_t xdiv, at::Tensor y, bool glu) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  check_cuda(eidx, "eidx");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 3 && y.dim() == 2, "expert_gemv: x [X, K], w [E, Nw, K], y [P, N]");
+  TORCH_CHECK(x.stride(1) == 1 && w.stride(2) == 1 && y.stride(1) == 1, "expert_gemv: unit inner strides required");
+  TORCH_CHECK(eidx.scalar_type() == at::kInt && eidx.dim() == 1 && eidx.is_contiguous(), "expert_gemv: eidx int32 [P]");
+  const int P = eidx.size(0), K = x.size(1), N = y.size(1);
+  TORCH_CHECK(xdiv >= 1 && y.size(0) == P && (P + xdiv - 1) / xdiv <= x.size(0), "expert_gemv: x/y rows vs pairs");
+  TORCH_CHECK(w.size(2) == K && w.size(1) == (glu ? 2 * N : N), "expert_gemv: weight shape mismatch");
+  TORCH_CHECK(K % 8 == 0 && x.stride(0) % 8 == 0 && w.stride(1) % 8 == 0 && w.stride(0) % 8 == 0,
+              "expert_gemv: K / leading dims must be multiples of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "expert_gemv: 16-byte aligned operands required");
+  TORCH_CHECK(P <= 65535, "expert_gemv: too many pairs");
+  if (P == 0) return;
+  check_rc(nxd::expert_gemv_launch(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(1), w.stride(0),
+                                   eidx.data_ptr<int32_t>(), P, (int)xdiv, y.data_ptr(), y.stride(0), N, K, glu,
+                                   cur_stream()),
+           "expert_gemv");
+}
+
 void dequant_int8(at::Tensor w, c10::optional<at::Tensor> scale, double tscale, at::Tensor out) {
   check_cuda(w, "w");
   TORCH_CHECK(w.scalar_type() == at::kChar && w.dim() == 2 && w.stride(1) == 1, "dequant: int8 [N, K] weight");
@@ -523,6 +549,7 @@ PYBIND11_MODULE(_C, m) {
   register_dataloader(m);
   m.def("gemv", &gemv);
   m.def("dequant_int8", &dequant_int8);
+  m.def("expert_gemv", &expert_gemv);
   m.doc() = "CDNA4 (gfx950) kernels of neuronx_distributed_llama3_2_amd";
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);

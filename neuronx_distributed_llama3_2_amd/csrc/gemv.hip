@@ -24,6 +24,11 @@ struct Params {
   uint16_t* y;
   int64_t ldy;
   int M, N, K;  // N = output columns (GLU: the up rows start at weight row N)
+  // expert (MoE decode) mode: blockIdx.y = (token, expert-slot) pair p; it multiplies x row
+  // p / xdiv with the weights of expert eidx[p] (base + eidx[p] * estride) into y row p
+  const int32_t* eidx;
+  int64_t estride;
+  int xdiv;
 };
 
 template <typename WT>
@@ -59,6 +64,12 @@ __global__ void __launch_bounds__(256) gemv_kernel(Params p) {
   const int wave = (blockIdx.x * 4) + (threadIdx.x >> 6);
   const int n0 = wave * ROWS;
   if (n0 >= p.N) return;
+  if (p.eidx) {
+    const int pair = blockIdx.y;
+    p.w = reinterpret_cast<const char*>(p.w) + (int64_t)p.eidx[pair] * p.estride * (int64_t)sizeof(WT);
+    p.x += (int64_t)(pair / p.xdiv) * p.ldx;
+    p.y += (int64_t)pair * p.ldy;
+  }
   int wrow[NW];
 #pragma unroll
   for (int r = 0; r < ROWS; ++r) {
@@ -133,10 +144,10 @@ __global__ void __launch_bounds__(256) dequant_kernel(const int8_t* __restrict__
 }
 
 template <typename WT, int MM, bool GLU>
-static int launch_m(const Params& p, hipStream_t s) {
+static int launch_m(const Params& p, hipStream_t s, int pairs = 1) {
   const int rows = p.N >= 8192 ? 2 : 1;
   const int waves = (p.N + rows - 1) / rows;
-  dim3 grid((waves + 3) / 4), block(256);
+  dim3 grid((waves + 3) / 4, pairs), block(256);
   if (rows == 2)
     hipLaunchKernelGGL((gemv_kernel<WT, MM, 2, GLU>), grid, block, 0, s, p);
   else
@@ -158,9 +169,19 @@ static int launch_t(const Params& p, hipStream_t s) {
 int gemv_launch(const void* x, int64_t ldx, const void* w, int64_t ldw, int w_is_int8, const float* scale, float tscale,
                 const void* bias, void* y, int64_t ldy, int M, int N, int K, int glu, hipStream_t stream) {
   gemv::Params p{reinterpret_cast<const uint16_t*>(x), ldx, w, ldw, scale, tscale,
-                 reinterpret_cast<const uint16_t*>(bias), reinterpret_cast<uint16_t*>(y), ldy, M, N, K};
+                 reinterpret_cast<const uint16_t*>(bias), reinterpret_cast<uint16_t*>(y), ldy, M, N, K,
+                 nullptr, 0, 1};
   if (w_is_int8) return glu ? gemv::launch_t<int8_t, true>(p, stream) : gemv::launch_t<int8_t, false>(p, stream);
   return glu ? gemv::launch_t<uint16_t, true>(p, stream) : gemv::launch_t<uint16_t, false>(p, stream);
+}
+
+// MoE decode: y[p, :N] = x[p / xdiv] . W[eidx[p]]^T  (W [E, Nw, K] bf16, rows ldw apart, experts
+// estride elements apart; GLU as above).  Only the selected experts' weights are read.
+int expert_gemv_launch(const void* x, int64_t ldx, const void* w, int64_t ldw, int64_t estride, const int32_t* eidx,
+                       int pairs, int xdiv, void* y, int64_t ldy, int N, int K, int glu, hipStream_t stream) {
+  gemv::Params p{reinterpret_cast<const uint16_t*>(x), ldx, w, ldw, nullptr, 1.f, nullptr,
+                 reinterpret_cast<uint16_t*>(y), ldy, 1, N, K, eidx, estride, xdiv};
+  return glu ? gemv::launch_m<uint16_t, 1, true>(p, stream, pairs) : gemv::launch_m<uint16_t, 1, false>(p, stream, pairs);
 }
 
 int dequant_int8_launch(const void* w, int64_t ldw, const float* scale, float tscale, void* out, int N, int K,

@@ -93,6 +93,24 @@ class _SubModel:
 
 
 class LlamaForCausalLMInference:
+    """Model family hooks (overridden by the MoE applications in inference/moe.py):
+    `_model_cls` the device module, `_hf_to_nxd` HF full state dict -> framework names,
+    `_config_from_dir` HF config.json -> model config."""
+
+    _model_cls = LlamaInferenceModel
+
+    @staticmethod
+    def _hf_to_nxd(hf_sd, model_config):
+        from ..models.llama.convert import hf_to_nxd
+
+        return hf_to_nxd(hf_sd, model_config)
+
+    @staticmethod
+    def _config_from_dir(path: str):
+        from .config import model_config_from_dir
+
+        return model_config_from_dir(path)
+
     def __init__(self, model_config, config: InferenceConfig, dtype: torch.dtype = torch.bfloat16,
                  device: Optional[torch.device] = None, init_weights: bool = True):
         self.model_config = model_config
@@ -106,7 +124,7 @@ class LlamaForCausalLMInference:
             if not ps.model_parallel_is_initialized():
                 _init_single_process()
                 ps.initialize_model_parallel(tensor_model_parallel_size=1)
-        self.model = LlamaInferenceModel(model_config, dtype=dtype,
+        self.model = self._model_cls(model_config, dtype=dtype,
                                          device=torch.device("meta") if not init_weights else self.device)
         if config.quantized:
             self._quantize()
@@ -139,16 +157,12 @@ class LlamaForCausalLMInference:
     def from_pretrained(cls, model_path: Optional[str], config: InferenceConfig, model_config=None,
                         dtype: torch.dtype = torch.bfloat16):
         """HF directory -> model on this rank's GPU (random init when model_path is None)."""
-        from .config import model_config_from_dir
-
         if model_config is None:
-            model_config = model_config_from_dir(model_path)
+            model_config = cls._config_from_dir(model_path)
         if model_path is None:
             return cls(model_config, config, dtype)
         self = cls(model_config, config, dtype, init_weights=False)
-        from ..models.llama.convert import hf_to_nxd
-
-        full = hf_to_nxd(load_hf_state_dict(model_path), model_config)
+        full = cls._hf_to_nxd(load_hf_state_dict(model_path), model_config)
         self._load_full(full)
         return self
 
@@ -175,6 +189,8 @@ class LlamaForCausalLMInference:
             raise RuntimeError(f"missing weights: {missing[:8]}")
         for p in self.model.parameters():
             p.requires_grad_(False)
+        if hasattr(self.model, "post_load"):
+            self.model.post_load()
         self.model.setup_kv_cache(self.max_batch, self.cache_len, self.device)
 
     def compile(self, serialize_base_path: str) -> None:
@@ -198,10 +214,8 @@ class LlamaForCausalLMInference:
     def load(cls, serialize_base_path: str, dtype: torch.dtype = torch.bfloat16):
         from safetensors.torch import load_file
 
-        from .config import model_config_from_dir
-
         config = InferenceConfig.from_pretrained(serialize_base_path)
-        model_config = model_config_from_dir(serialize_base_path)
+        model_config = cls._config_from_dir(serialize_base_path)
         self = cls(model_config, config, dtype, init_weights=False)
         rank = ps.get_tensor_model_parallel_rank()
         local = load_file(os.path.join(serialize_base_path, f"tp{rank}_sharded_checkpoint.safetensors"))

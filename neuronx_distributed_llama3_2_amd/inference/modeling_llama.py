@@ -1,210 +1,30 @@
 """Llama-3 / 3.1 / 3.2 inference model: tensor-parallel, persistent KV cache, fused CDNA4 kernels
-(reference: examples/inference/llama3/neuron_modeling_llama.py:117-446 and the device graph of
-examples/inference/modules/model_base.py:334-451).
+(reference: examples/inference/llama3/neuron_modeling_llama.py:117-446).
 
 The module IS the training `LlamaForCausalLM` (same parameter names, so training checkpoints and
-converted HF weights load directly) with an inference forward:
-
-* context encoding (prefill, T tokens per sequence): fused residual+RMSNorm kernel -> one fused
-  QKV GEMM -> in-place RoPE on the q/k columns of that buffer (one launch for both) -> in-place
-  KV-cache write -> causal flash attention (flash_attn_fwd.hip) on strided views -> o_proj
-  (+ TP all-reduce) -> add+norm -> gate_up GEMM -> SwiGLU kernel -> down (+ all-reduce); only the
-  last valid position of every sequence goes through the final norm and the lm_head;
-* token generation (T = 1, or T = speculation length): same block with the flash-decoding
-  kernel (inference.hip) reading the KV cache up to a per-sequence DEVICE length, so a decode
-  step has static shapes and no host sync — it is captured into hipGraphs (inference/graphs.py).
-
-KV cache: ONE allocation [layers, 2, max_batch, kv_heads_local, max_len, head_dim] (bf16);
-`seq_ids` selects cache rows (continuous batching).
+converted HF weights load directly) with the shared inference forward of `model_base` and a dense
+SwiGLU feed-forward: gate_up GEMM (or, at decode sizes, the skinny-GEMM kernel with SwiGLU fused
+into its epilogue) -> down projection (+ TP all-reduce).
 """
 
 from __future__ import annotations
 
 import copy
-import math
-from typing import Optional
 
 import torch
-import torch.distributed as dist
-import torch.nn.functional as F
 
-from .. import ops
-from ..ops.gemm import linear as _linear
-from ..ops.gemv import skinny_linear
 from ..models.llama.modeling_llama import LlamaForCausalLM
-from ..parallel_layers import parallel_state as ps
-from ..parallel_layers.parallel_state import get_tensor_model_parallel_size
+from .model_base import DecoderInferenceMixin
 
 
-class LlamaInferenceModel(LlamaForCausalLM):
+class LlamaInferenceModel(DecoderInferenceMixin, LlamaForCausalLM):
     def __init__(self, config, dtype=torch.bfloat16, device=None):
         cfg = copy.copy(config)
         cfg.sequence_parallel_enabled = False
-        super().__init__(cfg, dtype=dtype, device=device)
-        attn0 = self.model.layers[0].self_attn
-        self.nq, self.nkv, self.head_dim = attn0.num_heads_local, attn0.num_kv_heads_local, attn0.head_dim
-        self.tp = get_tensor_model_parallel_size()
-        self.kv_cache: Optional[torch.Tensor] = None
-        self.eps = float(config.rms_norm_eps)
-        self.eval()
-        for p in self.parameters():
-            p.requires_grad_(False)
+        LlamaForCausalLM.__init__(self, cfg, dtype=dtype, device=device)
+        self._init_inference(config)
 
-    # ------------------------------------------------------------------ KV cache
-    def setup_kv_cache(self, max_batch: int, max_len: int, device=None) -> torch.Tensor:
-        emb = self.model.embed_tokens.weight   # activation dtype (lm_head may be int8-quantized)
-        device = device or emb.device
-        L = len(self.model.layers)
-        shape = (L, 2, max_batch, self.nkv, max_len, self.head_dim)
-        if self.kv_cache is None or tuple(self.kv_cache.shape) != shape or self.kv_cache.device != torch.device(device):
-            self.kv_cache = torch.zeros(shape, dtype=emb.dtype, device=device)
-        return self.kv_cache
-
-    def reset_kv_cache(self) -> None:
-        if self.kv_cache is not None:
-            self.kv_cache.zero_()
-
-    # ------------------------------------------------------------------ collectives
-    def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
-        if self.tp > 1:
-            dist.all_reduce(x, group=ps.get_tensor_model_parallel_group())
-        return x
-
-    def _gather_vocab(self, logits: torch.Tensor) -> torch.Tensor:
-        if self.tp == 1:
-            return logits
-        from ..parallel import comm
-
-        out = torch.empty((self.tp,) + tuple(logits.shape), dtype=logits.dtype, device=logits.device)
-        comm.all_gather_into_tensor(out, logits.contiguous(), group=ps.get_tensor_model_parallel_group())
-        return torch.movedim(out, 0, -2).reshape(logits.shape[:-1] + (self.tp * logits.shape[-1],))
-
-    # ------------------------------------------------------------------ forward
-    @torch.no_grad()
-    def forward_tokens(self, input_ids: torch.Tensor, positions: torch.Tensor, seq_ids: Optional[torch.Tensor] = None,
-                       cache_len: Optional[torch.Tensor] = None, last_index: Optional[torch.Tensor] = None,
-                       prefill: bool = False, return_hidden: bool = False):
-        """input_ids [B, T]; positions [B, T] (int64) absolute positions of the new tokens;
-        seq_ids [B] cache rows; cache_len [B] int32 valid cache length AFTER this step (decode);
-        last_index [B] -> logits [B, V] of that token per sequence, else logits [B, T, V].
-        prefill=True: the new tokens start at position 0 (causal flash attention over them)."""
-        assert self.kv_cache is not None, "call setup_kv_cache() first"
-        B, T = input_ids.shape
-        nq, nkv, D = self.nq, self.nkv, self.head_dim
-        W = (nq + 2 * nkv) * D
-        cos_t, sin_t = self.model.rope_cache.tables(input_ids.device)
-        pos_flat = positions.reshape(-1)
-        pos0 = positions[:, 0].to(torch.int32)
-        sid32 = seq_ids.to(torch.int32) if seq_ids is not None else None   # once per step, not per layer
-        emb = self.model.embed_tokens
-        x = ops.vocab_parallel_embedding(input_ids, emb.weight, emb.start_index)
-        x = self._all_reduce(x)
-        residual = None
-        for i, layer in enumerate(self.model.layers):
-            attn, mlp = layer.self_attn, layer.mlp
-            h, residual = self._norm(x, layer.input_layernorm.weight, residual)
-            qkv = self._proj(attn.qkv_proj, h)  # [B, T, W]
-            ops.rope_inplace_(qkv.view(B * T, W), 0, nq + nkv, D, cos_t, sin_t, pos_flat)
-            q = qkv.view(B, T, nq + 2 * nkv, D)[:, :, :nq]
-            k = qkv.view(B, T, nq + 2 * nkv, D)[:, :, nq:nq + nkv]
-            v = qkv.view(B, T, nq + 2 * nkv, D)[:, :, nq + nkv:]
-            kc, vc = self.kv_cache[i, 0], self.kv_cache[i, 1]
-            ops.kv_cache_write(k, v, kc, vc, pos0, sid32)
-            if prefill:
-                o, _ = ops.flash_attn_fwd_lse(q, k, v, causal=True)
-            else:
-                o = ops.decode_attention(q, kc, vc, cache_len, sid32)
-            x = self._row(attn.o_proj, o.reshape(B, T, nq * D))
-            h, residual = self._norm(x, layer.post_attention_layernorm.weight, residual)
-            a = self._proj(mlp.gate_up_proj, h, glu=True)   # SwiGLU fused into the decode GEMV
-            x = self._row(mlp.down_proj, a)
-        if last_index is not None:
-            rows = torch.arange(B, device=x.device)
-            x = x[rows, last_index]
-            residual = residual[rows, last_index]
-        h, _ = self._norm(x, self.model.norm.weight, residual)
-        logits = self._gather_vocab(self._proj(self.lm_head, h))
-        return (logits, h) if return_hidden else logits
-
-    @torch.no_grad()
-    def forward_tree(self, tokens: torch.Tensor, positions: torch.Tensor, tree_mask: torch.Tensor, prefix_len: int,
-                     seq_id: int = 0):
-        """Medusa tree verification for ONE sequence: tokens / positions [N] (tree nodes at
-        prefix_len + depth), tree_mask [N, N] bool (node i sees node j iff j is i or an ancestor).
-        Every node also sees the cached prefix [0, prefix_len).  Nothing is written to the KV cache;
-        returns (logits [N, V], final hidden [N, H], per-layer (k, v) [N, Hkv, D] of the nodes) so
-        the caller commits only the accepted path (commit_tree_kv)."""
-        N = tokens.shape[0]
-        nq, nkv, D = self.nq, self.nkv, self.head_dim
-        g = nq // nkv
-        W = (nq + 2 * nkv) * D
-        cos_t, sin_t = self.model.rope_cache.tables(tokens.device)
-        scale = 1.0 / math.sqrt(D)
-        emb = self.model.embed_tokens
-        x = self._all_reduce(ops.vocab_parallel_embedding(tokens.view(1, N), emb.weight, emb.start_index))
-        residual = None
-        kvs = []
-        tree_bias = torch.zeros((N, N), dtype=torch.float32, device=tokens.device).masked_fill(~tree_mask, float("-inf"))
-        for i, layer in enumerate(self.model.layers):
-            attn, mlp = layer.self_attn, layer.mlp
-            h, residual = self._norm(x, layer.input_layernorm.weight, residual)
-            qkv = self._proj(attn.qkv_proj, h)
-            ops.rope_inplace_(qkv.view(N, W), 0, nq + nkv, D, cos_t, sin_t, positions.reshape(-1))
-            qkv4 = qkv.view(N, nq + 2 * nkv, D)
-            q, k, v = qkv4[:, :nq], qkv4[:, nq:nq + nkv], qkv4[:, nq + nkv:]
-            kvs.append((k.clone(), v.clone()))
-            kc = self.kv_cache[i, 0, seq_id, :, :prefix_len].float()   # [Hkv, P, D]
-            vc = self.kv_cache[i, 1, seq_id, :, :prefix_len].float()
-            qf = q.float().permute(1, 0, 2).reshape(nkv, g * N, D)    # heads grouped by kv head
-            s_c = torch.matmul(qf, kc.transpose(1, 2)) * scale         # [Hkv, g*N, P]
-            s_t = torch.matmul(qf, k.float().permute(1, 2, 0)) * scale  # [Hkv, g*N, N]
-            s_t = s_t.view(nkv, g, N, N) + tree_bias
-            s = torch.cat([s_c.view(nkv, g, N, prefix_len), s_t], -1)
-            p_ = torch.softmax(s, -1)
-            o = torch.matmul(p_[..., :prefix_len].reshape(nkv, g * N, prefix_len), vc) + \
-                torch.matmul(p_[..., prefix_len:].reshape(nkv, g * N, N), v.float().permute(1, 0, 2))
-            o = o.view(nq, N, D).permute(1, 0, 2).reshape(1, N, nq * D).to(x.dtype)
-            x = self._row(attn.o_proj, o)
-            h, residual = self._norm(x, layer.post_attention_layernorm.weight, residual)
-            x = self._row(mlp.down_proj, self._proj(mlp.gate_up_proj, h, glu=True))
-        h, _ = self._norm(x, self.model.norm.weight, residual)
-        logits = self._gather_vocab(self._proj(self.lm_head, h))
-        return logits.view(N, -1), h.view(N, -1), kvs
-
-    @torch.no_grad()
-    def commit_tree_kv(self, kvs, nodes: torch.Tensor, start: int, seq_id: int = 0) -> None:
-        """Write the K/V of the accepted tree nodes (in path order) at cache positions start..start+n."""
-        sid = torch.tensor([seq_id], dtype=torch.int32, device=nodes.device)
-        pos = torch.tensor([start], dtype=torch.int32, device=nodes.device)
-        for i, (k, v) in enumerate(kvs):
-            ops.kv_cache_write(k.index_select(0, nodes).unsqueeze(0), v.index_select(0, nodes).unsqueeze(0),
-                               self.kv_cache[i, 0], self.kv_cache[i, 1], pos, sid)
-
-    def _row(self, mod, x: torch.Tensor) -> torch.Tensor:
-        """Row-parallel projection: partial GEMM, TP all-reduce, then the (replicated) bias."""
-        y = self._all_reduce(self._proj(mod, x, use_bias=False))
-        b = getattr(mod, "bias", None)
-        return y + b if b is not None else y
-
-    @staticmethod
-    def _proj(mod, x: torch.Tensor, glu: bool = False, use_bias: bool = True) -> torch.Tensor:
-        """Local (no-collective) projection of a TP linear: bf16 or int8-quantized weights; decode-sized
-        inputs go through the skinny-GEMM kernel (int8 read directly, SwiGLU fused when glu=True)."""
-        if hasattr(mod, "_fused_weight_bias"):
-            w, b = mod._fused_weight_bias()
-        else:
-            w, b = mod.weight, getattr(mod, "bias", None)
-        if not use_bias:
-            b = None
-        scale = mod._row_scale() if w.dtype == torch.int8 else None
-        M = x.numel() // x.shape[-1]
-        if w.dtype == torch.int8 or (M <= 8 and x.is_cuda):
-            return skinny_linear(x, w, scale, b, glu=glu)
-        y = _linear(x, w, b)
-        return ops.swiglu(y) if glu else y
-
-    def _norm(self, x, w, residual):
-        if residual is None:
-            y, _ = ops.rms_norm(x, w, self.eps)
-            return y, x
-        return ops.rms_norm(x, w, self.eps, residual)
+    def _ffn(self, layer, h: torch.Tensor) -> torch.Tensor:
+        mlp = layer.mlp
+        a = self._proj(mlp.gate_up_proj, h, glu=True)   # SwiGLU fused into the decode GEMV
+        return self._row(mlp.down_proj, a)

@@ -29,6 +29,8 @@ Prompt = Union[str, Sequence[int]]
 
 
 class InferenceRunner:
+    app_cls = LlamaForCausalLMInference   # the inference application this runner drives
+
     def __init__(self, model_path: Optional[str] = None, tokenizer_path: Optional[str] = None,
                  generation_config: Optional[dict] = None):
         self.model_path = model_path
@@ -67,7 +69,7 @@ class InferenceRunner:
     def load_neuron_model_on_cpu(self, max_prompt_length: int, sequence_length: int, batch_size: int, **kwargs):
         cfg = self.get_config_for_nxd(batch_size, 1, max_prompt_length, sequence_length, **kwargs)
         cfg.use_hip_graphs = False
-        m = LlamaForCausalLMInference.from_pretrained(self.model_path, cfg, dtype=torch.float32)
+        m = self.app_cls.from_pretrained(self.model_path, cfg, dtype=torch.float32)
         return m
 
     def trace(self, traced_model_path: str, tp_degree: int = 1, batch_size: int = 1, max_prompt_length: int = 128,
@@ -76,7 +78,7 @@ class InferenceRunner:
         trace/compile step; kernels are prebuilt, graphs are captured at load)."""
         self.config = self.get_config_for_nxd(batch_size, tp_degree, max_prompt_length, sequence_length,
                                               enable_bucketing, **kwargs)
-        m = LlamaForCausalLMInference.from_pretrained(self.model_path, self.config)
+        m = self.app_cls.from_pretrained(self.model_path, self.config)
         m.compile(traced_model_path)
         if self.tokenizer_path and os.path.isdir(self.tokenizer_path):
             tok = self.load_tokenizer()
@@ -84,7 +86,7 @@ class InferenceRunner:
                 tok.save_pretrained(traced_model_path)
 
     def load_neuron_model(self, traced_model_path: str):
-        m = LlamaForCausalLMInference.load(traced_model_path)
+        m = self.app_cls.load(traced_model_path)
         self.config = m.config
         return m
 

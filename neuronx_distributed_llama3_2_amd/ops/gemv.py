@@ -62,3 +62,29 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, scale: Optional[torch.Tensor
 
         y = swiglu(y)
     return y
+
+
+def expert_linear(x: torch.Tensor, w_t: torch.Tensor, eidx: torch.Tensor, xdiv: int = 1,
+                  glu: bool = False) -> torch.Tensor:
+    """MoE decode projection for P (token, expert-slot) pairs: y[p] = x[p // xdiv] @ W[eidx[p]]^T,
+    W given output-major as w_t [E, Nw, K]; glu=True: rows [gate; up] -> silu(gate) * up.  Reads
+    only the selected experts' weights (csrc/gemv.hip expert mode); static shapes, no host sync,
+    so it is captured in the decode hipGraph."""
+    P = eidx.numel()
+    Nw, K = w_t.shape[1], w_t.shape[2]
+    N = Nw // 2 if glu else Nw
+    if use_native(x, w_t) and x.dtype == torch.bfloat16 and w_t.dtype == torch.bfloat16 and w_t.stride(2) == 1 \
+            and K % 8 == 0 and w_t.stride(1) % 8 == 0 and w_t.stride(0) % 8 == 0 and w_t.data_ptr() % 16 == 0:
+        x2 = x.reshape(-1, K)
+        if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+            x2 = x2.contiguous()
+        y = torch.empty((P, N), dtype=torch.bfloat16, device=x.device)
+        ext().expert_gemv(x2, w_t, eidx.reshape(-1).to(torch.int32).contiguous(), int(xdiv), y, glu)
+        return y
+    rows = x.reshape(-1, K).index_select(0, torch.arange(P, device=x.device) // xdiv)
+    y = torch.bmm(rows.unsqueeze(1), w_t.index_select(0, eidx.reshape(-1).long()).transpose(1, 2)).squeeze(1)
+    if glu:
+        from .activations import swiglu
+
+        y = swiglu(y)
+    return y

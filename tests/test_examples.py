@@ -76,3 +76,35 @@ def test_inference_runner_cli_trace_generate_check(tmp_path):
     assert cli.main(["check_accuracy"] + base + ["--prompt_ids", "5,6,7,8,9,10"]) is True
     rep = cli.main(["benchmark"] + base + ["--num_runs", "2"])
     assert "e2e_model" in rep and rep["e2e_model"]["latency_ms_p50"] > 0
+
+
+def test_moe_and_quantized_inference_clis(tmp_path):
+    """examples/inference/run_dbrx.py and run_llama_quantized.py: trace an HF directory, reload,
+    generate (reference examples E10/E11: run_dbrx.py, run_llama_quantized.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "examples", "inference"))
+    import run_dbrx  # noqa: F401  (module import = the CLI wiring is valid)
+    import run_llama_quantized
+    from llama3_2_runner import main as runner_main
+    from transformers import DbrxConfig, DbrxForCausalLM, LlamaConfig, LlamaForCausalLM
+
+    from neuronx_distributed_llama3_2_amd.inference.moe import DbrxRunner
+
+    torch.manual_seed(0)
+    dbrx = DbrxForCausalLM(DbrxConfig(d_model=64, n_heads=4, n_layers=1, max_seq_len=128, vocab_size=128,
+                                      attn_config=dict(kv_n_heads=2, clip_qkv=8.0, rope_theta=10000.0),
+                                      ffn_config=dict(ffn_hidden_size=64, moe_num_experts=4, moe_top_k=2)))
+    src = str(tmp_path / "dbrx")
+    dbrx.save_pretrained(src)
+    traced = str(tmp_path / "dbrx_traced")
+    runner_main(["trace", "--model_path", src, "--traced_path", traced, "--max_prompt_length", "16",
+                 "--sequence_length", "24"], runner_cls=DbrxRunner)
+    out = runner_main(["generate", "--traced_path", traced, "--prompt_ids", "3,4,5"], runner_cls=DbrxRunner)
+    assert out.shape == (1, 24)
+    llama = LlamaForCausalLM(LlamaConfig(hidden_size=64, intermediate_size=128, num_hidden_layers=1,
+                                         num_attention_heads=4, num_key_value_heads=2, vocab_size=128,
+                                         max_position_embeddings=128))
+    lsrc = str(tmp_path / "llama")
+    llama.save_pretrained(lsrc)
+    q = run_llama_quantized.main(["--model_path", lsrc, "--traced_path", str(tmp_path / "q"), "--max_prompt_length",
+                                  "16", "--sequence_length", "24", "--prompt_ids", "7,8,9"])
+    assert q.shape == (1, 24)
