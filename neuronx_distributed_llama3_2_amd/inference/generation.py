@@ -125,7 +125,7 @@ class LlamaForCausalLMInference:
                 _init_single_process()
                 ps.initialize_model_parallel(tensor_model_parallel_size=1)
         self.model = self._model_cls(model_config, dtype=dtype,
-                                         device=torch.device("meta") if not init_weights else self.device)
+                                     device=torch.device("meta") if not init_weights else self.device)
         if config.quantized:
             self._quantize()
         self.max_batch = config.max_batch_size
@@ -267,15 +267,21 @@ class LlamaForCausalLMInference:
     __call__ = forward
 
     # ------------------------------------------------------------------ generation
+    def _decode_state(self, batch: int) -> DecodeState:
+        st = self._states.get(batch)
+        if st is None:
+            steps_cap = (math.ceil(self.config.max_length / self.graph_steps) + 1) * self.graph_steps
+            st = self._states[batch] = DecodeState(batch, steps_cap, self.device)
+        return st
+
     def _graph(self, batch: int, sampler: Sampler) -> DecodeGraph:
+        """Decode graph of (batch, sampler).  Call with the state already loaded: the capture's
+        eager warm-up then writes the KV cache only at positions the replay overwrites before it
+        reads them (a stale state would overwrite the freshly prefilled prompt positions)."""
         key = (batch, sampler.top_k, sampler.temperature)
         g = self._graphs.get(key)
         if g is None:
-            st = self._states.get(batch)
-            if st is None:
-                steps_cap = (math.ceil(self.config.max_length / self.graph_steps) + 1) * self.graph_steps
-                st = self._states[batch] = DecodeState(batch, steps_cap, self.device)
-            g = self._graphs[key] = DecodeGraph(self.model, sampler, st, self.graph_steps,
+            g = self._graphs[key] = DecodeGraph(self.model, sampler, self._decode_state(batch), self.graph_steps,
                                                 use_graph=self.config.use_hip_graphs)
         return g
 
@@ -332,10 +338,10 @@ class LlamaForCausalLMInference:
         new = [first.view(B, 1)]
         if max_new_tokens > 1:
             Bp = B
-            g = self._graph(Bp, sampler)
-            st = g.state
+            st = self._decode_state(Bp)
             uni = torch.rand((st.max_steps, Bp), device=dev, generator=gen)
             st.load(first, lengths, torch.arange(Bp, device=dev), uni)
+            g = self._graph(Bp, sampler)
             todo = max_new_tokens - 1
             done_steps = 0
             while done_steps < todo:

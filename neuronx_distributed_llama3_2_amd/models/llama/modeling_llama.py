@@ -240,6 +240,10 @@ def llama_config(name: str = "llama3-8b", **overrides):
         "llama2-7b": dict(hidden_size=4096, intermediate_size=11008, num_hidden_layers=32, num_attention_heads=32,
                           num_key_value_heads=32, vocab_size=32000, rope_theta=10000.0, max_position_embeddings=4096,
                           rms_norm_eps=1e-5),
+        # CodeGen2.5-7B is a Llama-architecture model (reference: examples/training/codegen25/config.json)
+        "codegen25-7b": dict(hidden_size=4096, intermediate_size=11008, num_hidden_layers=32, num_attention_heads=32,
+                             num_key_value_heads=32, vocab_size=51200, rope_theta=10000.0,
+                             max_position_embeddings=2048, rms_norm_eps=1e-6),
         "tiny": dict(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
                      num_key_value_heads=2, vocab_size=1024, rope_theta=10000.0, max_position_embeddings=512,
                      rms_norm_eps=1e-5),

@@ -15,7 +15,7 @@ import time
 from collections import deque
 from dataclasses import dataclass, field
 from itertools import chain
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, Iterable, List, Optional
 
 import torch
 from torch.optim.lr_scheduler import LambdaLR
@@ -208,3 +208,54 @@ def create_partition(num_hidden_layers: int, pipeline_parallel_size: int) -> Lis
 def get_dtype(model) -> str:
     p = next(model.parameters())
     return str(p.dtype).replace("torch.", "")
+
+
+def sample_num_spans(rng, max_num_spans: int = 16) -> int:
+    """1 + Poisson(1) spans, capped (reference: examples/training/codegen25/get_dataset_infill.py:35-39)."""
+    return int(min(int(rng.poisson(1.0)) + 1, max_num_spans))
+
+
+def format_to_infill(tokens: List[int], num_spans: int, mask_ids: List[int], eom_id: int, sep_ids: List[int],
+                     rng) -> Optional[List[int]]:
+    """Causal-infilling ("fill in the middle") rewrite of one token sequence, CodeGen2.5 style:
+    `prefix-with-<mask_i>-holes ++ sep_ids ++ (<mask_i> span_i <eom>)...`.  Spans are sampled left to
+    right, at least one token apart; returns None when the sequence is too short for `num_spans`.
+    Token ids instead of a tokenizer (reference behaviour: get_dataset_infill.py:42-90)."""
+    max_len = (len(tokens) - num_spans) // num_spans
+    if max_len <= 0 or num_spans > len(mask_ids):
+        return None
+    start_lo, end_hi = 1, max_len
+    prefix: List[int] = []
+    suffix: List[int] = []
+    for i in range(num_spans):
+        n = int(rng.integers(1, max_len + 1))
+        start = int(rng.integers(start_lo, end_hi - n + 2))
+        span = tokens[start:start + n]
+        prefix += tokens[start_lo - 1:start] + [mask_ids[i]]
+        suffix += [mask_ids[i]] + span + [eom_id]
+        start_lo, end_hi = start + n + 1, start + n + max_len
+        if i == num_spans - 1:
+            prefix += tokens[start + n:]
+    return prefix + list(sep_ids) + suffix
+
+
+def infill_token_blocks(blocks: Iterable[List[int]], block_size: int, mask_ids: List[int], eom_id: int,
+                        sep_ids: List[int], seed: int = 42, fraction: float = 0.5,
+                        max_num_spans: int = 16) -> List[List[int]]:
+    """Apply `format_to_infill` to `fraction` of the blocks, keeping every block at `block_size`
+    tokens: each span adds two masks and one <eom>, so only the first block_size - extra tokens are
+    rewritten (reference: get_dataset_infill.py:103-137)."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for b in blocks:
+        b = list(b)
+        if rng.random() < fraction:
+            k = sample_num_spans(rng, max_num_spans)
+            extra = 3 * k + len(sep_ids)
+            filled = format_to_infill(b[:block_size - extra], k, mask_ids, eom_id, sep_ids, rng)
+            if filled is not None:
+                b = (filled + b[block_size - extra:])[:block_size]
+        out.append(b[:block_size])
+    return out

@@ -108,3 +108,62 @@ def test_moe_and_quantized_inference_clis(tmp_path):
     q = run_llama_quantized.main(["--model_path", lsrc, "--traced_path", str(tmp_path / "q"), "--max_prompt_length",
                                   "16", "--sequence_length", "24", "--prompt_ids", "7,8,9"])
     assert q.shape == (1, 24)
+
+
+def test_infill_transform_and_codegen_data_script(tmp_path):
+    """CodeGen2.5 causal-infilling rewrite (reference: codegen25/get_dataset_infill.py): every
+    masked span reappears after the separator, in order, terminated by <eom>; blocks keep their size."""
+    import numpy as np
+
+    from neuronx_distributed_llama3_2_amd.utils.training_utils import format_to_infill, infill_token_blocks
+
+    MASKS, EOM, SEP = [1001, 1002, 1003], 1010, [1020, 1021]
+    toks = list(range(40))
+    out = format_to_infill(toks, 2, MASKS, EOM, SEP, np.random.default_rng(0))
+    s = out.index(SEP[0])
+    prefix, suffix = out[:s], out[s + 2:]
+    assert prefix.count(MASKS[0]) == 1 and prefix.count(MASKS[1]) == 1
+    spans = []
+    for m in MASKS[:2]:
+        i = suffix.index(m)
+        j = suffix.index(EOM, i)
+        spans.append(suffix[i + 1:j])
+    # prefix with each hole filled by its span restores the original sequence
+    rebuilt = []
+    for t in prefix:
+        rebuilt += spans[MASKS.index(t)] if t in MASKS else [t]
+    assert rebuilt == toks
+    assert format_to_infill(toks[:3], 3, MASKS, EOM, SEP, np.random.default_rng(0)) is None
+    blocks = infill_token_blocks([list(range(64)) for _ in range(10)], 64, MASKS, EOM, SEP, seed=1)
+    assert all(len(b) == 64 for b in blocks) and any(SEP[0] in b for b in blocks)
+    sys.path.insert(0, os.path.join(ROOT, "examples", "training", "codegen25"))
+    import get_dataset_infill
+
+    from neuronx_distributed_llama3_2_amd.utils.data_loader import write_token_file
+
+    src = str(tmp_path / "toks.bin")
+    write_token_file(src, [np.arange(32 * 8) % 500])
+    res = get_dataset_infill.main(["--input", src, "--output", str(tmp_path / "inf.bin"), "--block_size", "32",
+                                   "--mask_ids", "1001,1002", "--eom_id", "1010", "--sep_ids", "1020,1021"])
+    assert len(res) == 8 and np.fromfile(str(tmp_path / "inf.bin"), dtype=np.uint32).size == 256
+
+
+def _w_family(rank, world, out_dir, family, extra):
+    sys.path.insert(0, os.path.join(ROOT, "examples", "training", "llama"))
+    import tp_zero1_llama_hf_pretrain as ex
+
+    argv = ["--model_family", family, "--model_path", "tiny", "--tensor_parallel_size", "2", "--seq_len", "32",
+            "--batch_size", "1", "--max_steps", "3", "--use_zero_1", "--sequence_parallel_enabled", "--output_dir",
+            out_dir, "--lr", "1e-3", "--warmup_steps", "1"] + extra
+    loss = ex.main(argv)
+    if rank == 0:
+        torch.save(float(loss), os.path.join(out_dir, f"{family}.pt"))
+
+
+def test_pretrain_example_mixtral_and_neox_families(tmp_path):
+    """The pre-training example drives the other model families (reference examples E4 Mixtral,
+    E5 GPT-NeoX) with TP=2 + SP + ZeRO-1 on gloo."""
+    for fam, extra in (("mixtral", []), ("gpt_neox", [])):
+        run_distributed(_w_family, 2, str(tmp_path), fam, extra)
+        loss = torch.load(str(tmp_path / f"{fam}.pt"))
+        assert loss == loss and loss < 20.0
