@@ -31,6 +31,7 @@ from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedP
 from neuronx_distributed_llama3_2_amd.parallel.grad_buffer import find_shared_params  # noqa: E402
 from neuronx_distributed_llama3_2_amd.parallel_layers import parallel_state as ps  # noqa: E402
 from neuronx_distributed_llama3_2_amd.parallel_layers.random import model_parallel_manual_seed  # noqa: E402
+from neuronx_distributed_llama3_2_amd.utils.profiling import llama_num_params, mfu, model_flops_per_token  # noqa: E402
 
 BASELINE_TOKENS_PER_S = None  # the reference publishes no Llama-3-8B throughput
 
@@ -119,6 +120,8 @@ def main():
     value = tokens / el
     if rank == 0:
         mem = torch.cuda.max_memory_allocated(dev) / 2**30 if use_cuda else 0.0
+        nparams = llama_num_params(cfg)
+        fpt = model_flops_per_token(nparams, cfg.num_hidden_layers, cfg.hidden_size, a.seq)
         par = f"tp{tp}" + ("_sp" if over["sequence_parallel_enabled"] else "") + (f"_dp{dp}_zero1" if dp > 1 else "")
         rec = {
             "metric": "tokens/sec (whole node) Llama-3-8B TP=8 bf16 training at 1/2/4/8 MI355X",
@@ -139,6 +142,8 @@ def main():
                        "activation_checkpoint": a.ckpt or "none"},
             "loss": round(float(loss.item()), 4),
             "params_per_rank": nparams_local,
+            "model_params": nparams,
+            "mfu": round(mfu(value, fpt, world), 4),   # vs 2.5 PFLOP/s dense bf16 per GPU
             "peak_mem_gib": round(mem, 1),
         }
         print(json.dumps(rec), flush=True)

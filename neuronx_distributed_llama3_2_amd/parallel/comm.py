@@ -6,6 +6,12 @@ contiguous buffers: `all_gather_into_tensor`, `reduce_scatter_tensor`, `all_redu
 overlap communication with compute (the collective runs on RCCL's internal stream and the
 consumer waits on it before use).
 
+Stream-ordering debug mode (`NXD_COMM_DEBUG=1` or `set_comm_debug(True)`): every
+async handle is registered with its op, shape and call site until `.wait()`; `assert_no_pending_
+collectives(where)` (called by the gradient buffer once backward's reductions are drained) fails
+with the list of collectives that were launched but never waited on — the use-before-wait /
+leaked-handle class of bugs that otherwise shows up as silent corruption or a hang at exit.
+
 The gloo backend (CPU test harness) lacks the "_base" flat-tensor collectives; the same calls are
 emulated there with list all-gathers / all-reduce + slice, so the parallel code paths are the same
 on CPU and GPU.
@@ -13,10 +19,64 @@ on CPU and GPU.
 
 from __future__ import annotations
 
-from typing import List, Optional
+import itertools
+import os
+import traceback
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
+
+_debug = os.environ.get("NXD_COMM_DEBUG", "0") == "1"
+_pending: Dict[int, str] = {}
+_ids = itertools.count()
+
+
+def set_comm_debug(enabled: bool) -> None:
+    global _debug
+    _debug = bool(enabled)
+    _pending.clear()
+
+
+def comm_debug_enabled() -> bool:
+    return _debug
+
+
+class _Tracked:
+    """Async work handle registered in the pending table until waited on."""
+
+    def __init__(self, work, key):
+        self._work, self._key = work, key
+
+    def wait(self, *a, **k):
+        r = self._work.wait(*a, **k) if self._work is not None else True
+        _pending.pop(self._key, None)
+        return r
+
+    def is_completed(self):
+        return self._work.is_completed() if self._work is not None else True
+
+    def __getattr__(self, name):
+        return getattr(self._work, name)
+
+
+def _track(work, op: str, t: torch.Tensor):
+    if not _debug:
+        return work
+    key = next(_ids)
+    site = traceback.extract_stack(limit=4)[0]
+    _pending[key] = f"{op}{tuple(t.shape)} {t.dtype} from {os.path.basename(site.filename)}:{site.lineno}"
+    return _Tracked(work, key)
+
+
+def pending_collectives() -> List[str]:
+    return list(_pending.values())
+
+
+def assert_no_pending_collectives(where: str) -> None:
+    if _debug and _pending:
+        raise AssertionError(f"{where}: {len(_pending)} async collective(s) never waited on: "
+                             + "; ".join(_pending.values()))
 
 
 class _Done:
@@ -37,7 +97,8 @@ def _is_gloo(group) -> bool:
 def all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
     """out[i*n:(i+1)*n] = inp of rank i (dim 0)."""
     if not _is_gloo(group):
-        return dist.all_gather_into_tensor(out, inp.contiguous(), group=group, async_op=async_op)
+        w = dist.all_gather_into_tensor(out, inp.contiguous(), group=group, async_op=async_op)
+        return _track(w, "all_gather", out) if async_op else w
     ws = dist.get_world_size(group=group)
     chunks = list(out.chunk(ws, dim=0))
     src = inp.detach().contiguous().cpu()   # gloo gathers host tensors (GPU tensors are staged)
@@ -45,36 +106,39 @@ def all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, asy
     dist.all_gather(tmp, src, group=group)
     for c, t in zip(chunks, tmp):
         c.copy_(t)
-    return _Done() if async_op else None
+    return _track(_Done(), "all_gather", out) if async_op else None
 
 
 def reduce_scatter_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False,
                           op=dist.ReduceOp.SUM):
     """out = sum over ranks of inp[rank*n:(rank+1)*n] (dim 0)."""
     if not _is_gloo(group):
-        return dist.reduce_scatter_tensor(out, inp.contiguous(), op=op, group=group, async_op=async_op)
+        w = dist.reduce_scatter_tensor(out, inp.contiguous(), op=op, group=group, async_op=async_op)
+        return _track(w, "reduce_scatter", inp) if async_op else w
     ws = dist.get_world_size(group=group)
     r = dist.get_rank(group=group)
     full = inp.contiguous().clone()
     dist.all_reduce(full, op=op, group=group)
     out.copy_(full.chunk(ws, dim=0)[r])
-    return _Done() if async_op else None
+    return _track(_Done(), "reduce_scatter", inp) if async_op else None
 
 
 def all_reduce(t: torch.Tensor, group=None, async_op: bool = False, op=dist.ReduceOp.SUM):
-    return dist.all_reduce(t, op=op, group=group, async_op=async_op)
+    w = dist.all_reduce(t, op=op, group=group, async_op=async_op)
+    return _track(w, "all_reduce", t) if async_op else w
 
 
 def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
     if not _is_gloo(group):
-        return dist.all_to_all_single(out, inp.contiguous(), group=group, async_op=async_op)
+        w = dist.all_to_all_single(out, inp.contiguous(), group=group, async_op=async_op)
+        return _track(w, "all_to_all", inp) if async_op else w
     ws = dist.get_world_size(group=group)
     ins = list(inp.contiguous().chunk(ws, dim=0))
     outs = [torch.empty_like(c) for c in ins]
     _a2a_via_gather(outs, ins, group)
     for o, c in zip(out.chunk(ws, dim=0), outs):
         o.copy_(c)
-    return _Done() if async_op else None
+    return _track(_Done(), "all_to_all", inp) if async_op else None
 
 
 def _a2a_via_gather(outs: List[torch.Tensor], ins: List[torch.Tensor], group):

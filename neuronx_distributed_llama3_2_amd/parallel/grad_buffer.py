@@ -162,7 +162,7 @@ class FlatBuffer:
             b.out = self.grad_data[b.start + self.dp_rank * n: b.start + (self.dp_rank + 1) * n]
             b.handle = comm.reduce_scatter_tensor(b.out, g, group=self.dp_group, async_op=True)
         else:
-            b.handle = dist.all_reduce(g, group=self.dp_group, async_op=True)
+            b.handle = comm.all_reduce(g, group=self.dp_group, async_op=True)
 
     def finish_grad_sync(self, average: bool = True) -> None:
         """Launch any bucket not yet launched, wait for all, average over DP."""
@@ -181,6 +181,7 @@ class FlatBuffer:
                     b.out.div_(self.dp)
                 else:
                     self.grad_data[b.start:b.end].div_(self.dp)
+        comm.assert_no_pending_collectives("finish_grad_sync")
 
     # ---------------------------------------------------------------- ZeRO-1 views
     def shard_ranges(self) -> List[Tuple[int, int]]:
@@ -205,6 +206,7 @@ class FlatBuffer:
             handles.append(comm.all_gather_into_tensor(full, mine, group=self.dp_group, async_op=True))
         for h in handles:
             h.wait()
+        comm.assert_no_pending_collectives("gather_params")
 
     def zero_grad(self) -> None:
         self.grad_data.zero_()

@@ -34,6 +34,7 @@ from ..parallel_layers.parallel_state import (
 )
 from ..parallel_layers.utils import move_all_tensor_to_cpu
 from ..utils.logger import get_logger
+from ..utils.resilience import fault_point
 from ..utils.serialization import xser_load, xser_save
 from .checkpoint_storage import BaseCheckpointStorage, FilesysCheckpointStorage, create_checkpoint_storage
 
@@ -66,18 +67,36 @@ def _global_rank() -> int:
     return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
 
 
-def _determine_remove_tags(checkpoint_dir: BaseCheckpointStorage, num_kept: Optional[int]) -> List[str]:
+def _determine_remove_tags(checkpoint_dir: BaseCheckpointStorage, num_kept: Optional[int],
+                           current: Optional[str] = None) -> List[str]:
+    """Tags to delete: every tag without its `done` marker other than the one being written
+    (interrupted saves and interrupted deletions — the reference only catches the latter,
+    trainer/checkpoint.py:62-89) plus the oldest completed tags beyond `num_kept`."""
     tags = checkpoint_dir.list_checkpoint_tags()
     corrupted, completed = [], []
     for tag in tags:
         if checkpoint_dir.file_exists(os.path.join(tag, "done")):
             completed.append(tag)
-        elif not completed:
-            corrupted.append(tag)  # interrupted deletion (older than a completed tag)
+        elif tag != current:
+            corrupted.append(tag)
     remove = corrupted
     if num_kept is not None and num_kept != -1 and len(completed) > num_kept:
         remove += completed[: len(completed) - num_kept]
     return remove
+
+
+def _snapshot(data: Any) -> Any:
+    """Host copy that training can no longer mutate: device tensors are copied to the host, host
+    tensors are cloned (`.cpu()` of a host tensor aliases it, and the async writer thread would
+    otherwise serialise a state the next optimizer steps are already changing)."""
+    if isinstance(data, torch.Tensor):
+        t = data.detach()
+        return t.clone() if t.device.type == "cpu" else t.cpu()
+    if isinstance(data, dict):
+        return {k: _snapshot(v) for k, v in data.items()}
+    if isinstance(data, (list, tuple)):
+        return type(data)(_snapshot(v) for v in data)
+    return data
 
 
 class CheckpointIOState:
@@ -93,8 +112,8 @@ class CheckpointIOState:
 
     def wait_save(self) -> None:
         if self.pending is not None:
-            self.pending.result()  # re-raises a failed async save
-            self.pending = None
+            fut, self.pending = self.pending, None
+            fut.result()  # re-raises a failed async save (once; its tag never gets `done`)
 
     def begin(self, storage: BaseCheckpointStorage, tag: str) -> None:
         self.wait_save()
@@ -107,7 +126,7 @@ class CheckpointIOState:
         self.tasks = []
 
     def add_save_task(self, obj: Any, filename: str, xser: bool = False) -> None:
-        self.tasks.append((move_all_tensor_to_cpu(obj), filename, xser))
+        self.tasks.append((_snapshot(obj) if self.async_save else move_all_tensor_to_cpu(obj), filename, xser))
 
     def _run(self, tasks, storage):
         for obj, fn, xser in tasks:
@@ -117,12 +136,14 @@ class CheckpointIOState:
                 xser_save(obj, path)
             else:
                 storage.save_object(obj, fn)
+            fault_point("ckpt_after_shard_write")
 
     def _finish(self, storage, tag, num_kept):
         _barrier()
         if _global_rank() == 0:
+            fault_point("ckpt_before_done")
             storage.save_text("1", os.path.join(tag, "done"))
-            for t in _determine_remove_tags(storage, num_kept):
+            for t in _determine_remove_tags(storage, num_kept, current=tag):
                 if t != tag:
                     storage.remove_dir(t)
 
