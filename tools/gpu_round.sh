@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out/round
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/round/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/round/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/round/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/round/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc" >> gpurun_out/round/smoke.log; [ $rc -ne 0 ] && exit $rc
