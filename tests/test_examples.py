@@ -167,3 +167,55 @@ def test_pretrain_example_mixtral_and_neox_families(tmp_path):
         run_distributed(_w_family, 2, str(tmp_path), fam, extra)
         loss = torch.load(str(tmp_path / f"{fam}.pt"))
         assert loss == loss and loss < 20.0
+
+
+def _w_pp_pretrain(rank, world, out_dir, cfg_path, steps_this_run):
+    sys.path.insert(0, os.path.join(ROOT, "examples", "training", "llama"))
+    import tp_pp_llama_hf_pretrain as ex
+
+    argv = ["--model_path", cfg_path, "--tensor_parallel_size", "2", "--pipeline_parallel_size", "2",
+            "--num_microbatches", "2", "--train_batch_size", "4", "--seq_len", "32", "--max_steps", "4",
+            "--steps_this_run", str(steps_this_run), "--use_zero_1", "--sequence_parallel_enabled",
+            "--checkpoint_dir", os.path.join(out_dir, "ckpt"), "--checkpoint_freq", "2", "--output_dir", out_dir,
+            "--lr", "1e-3", "--warmup_steps", "1", "--watchdog_timeout", "600"]
+    loss = ex.main(argv)
+    if rank == 0:
+        torch.save(float(loss), os.path.join(out_dir, f"pp_loss_{steps_this_run}.pt"))
+
+
+def test_llama_tp_pp_example_resume(tmp_path):
+    """examples/training/llama/tp_pp_llama_hf_pretrain.py (reference E2): TP2 x PP2 1F1B with ZeRO-1
+    and SP on 4 gloo ranks, checkpoint at step 2, resume to step 4."""
+    from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import llama_config
+
+    cfg = llama_config("tiny", num_hidden_layers=4, hidden_size=64, intermediate_size=128, vocab_size=256,
+                       num_attention_heads=4, num_key_value_heads=2)
+    cfg_path = str(tmp_path / "config.json")
+    with open(cfg_path, "w") as f:
+        json.dump(cfg.to_dict(), f)
+    run_distributed(_w_pp_pretrain, 4, str(tmp_path), cfg_path, 2)
+    assert os.path.exists(tmp_path / "ckpt" / "step_2" / "done")
+    run_distributed(_w_pp_pretrain, 4, str(tmp_path), cfg_path, 2)
+    assert os.path.exists(tmp_path / "ckpt" / "step_4" / "done")
+    assert torch.isfinite(torch.tensor(torch.load(tmp_path / "pp_loss_2.pt")))
+    m = json.load(open(tmp_path / "results.json"))
+    assert m["results"]["parameters"]["pipeline_parallel_size"] == 2
+
+
+def _w_bert(rank, world, out_dir):
+    sys.path.insert(0, os.path.join(ROOT, "examples", "training", "bert"))
+    import tp_dp_bert_hf_pretrain as ex
+
+    loss = ex.main(["--model", "tiny", "--tensor_parallel_size", "2", "--batch_size", "4", "--seq_len", "32",
+                    "--max_steps", "6", "--warmup_steps", "1", "--lr", "2e-3", "--output_dir", out_dir,
+                    "--grad_accum_usteps", "2"])
+    if rank == 0:
+        torch.save(float(loss), os.path.join(out_dir, "bert_loss.pt"))
+
+
+def test_bert_tp_dp_example(tmp_path):
+    """examples/training/bert/tp_dp_bert_hf_pretrain.py (reference E6): TP2 x DP2 MLM+NSP."""
+    run_distributed(_w_bert, 4, str(tmp_path))
+    assert torch.isfinite(torch.tensor(torch.load(tmp_path / "bert_loss.pt")))
+    m = json.load(open(tmp_path / "results.json"))
+    assert {x["MetricName"] for x in m["results"]["metrics"]} >= {"Final loss", "Average throughput"}
