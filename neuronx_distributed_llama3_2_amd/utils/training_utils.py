@@ -259,3 +259,38 @@ def infill_token_blocks(blocks: Iterable[List[int]], block_size: int, mask_ids: 
                 b = (filled + b[block_size - extra:])[:block_size]
         out.append(b[:block_size])
     return out
+
+
+# ------------------------------------------------------------------ instruction fine-tuning data
+def format_instruction(sample: Dict[str, Any], with_answer: bool = True) -> str:
+    """Dolly-style prompt (reference: examples/training/llama/training_utils.py:130-207):
+    '### Instruction' / optional '### Context' / '### Answer' sections joined by newlines."""
+    parts = [f"### Instruction\n{sample['instruction']}"]
+    if sample.get("context"):
+        parts.append(f"### Context\n{sample['context']}")
+    parts.append(f"### Answer\n{sample['response']}" if with_answer else "### Answer\n")
+    return "\n".join(parts)
+
+
+def build_instruction_datasets(records: List[Dict[str, Any]], tokenizer, chunk_length: int = 2048,
+                               test_size: int = 8, seed: int = 0):
+    """-> (train windows, test examples).
+
+    Train: every record rendered with its answer + EOS, tokenized, concatenated and cut into
+    `chunk_length` windows (labels = inputs; the tail shorter than a window is dropped).
+    Test (the last `test_size` records of a seeded shuffle): prompt ids without the answer and the
+    answer ids as labels, for response-only loss / generation checks."""
+    import random
+
+    recs = list(records)
+    random.Random(seed).shuffle(recs)
+    test, train = recs[len(recs) - test_size:] if test_size else [], recs[:len(recs) - test_size]
+    eos = tokenizer.eos_token or ""
+    stream: List[int] = []
+    for r in train:
+        stream += tokenizer(format_instruction(r) + eos)["input_ids"]
+    n = (len(stream) // chunk_length) * chunk_length
+    windows = [stream[i:i + chunk_length] for i in range(0, n, chunk_length)]
+    tests = [{"input_ids": tokenizer(format_instruction(r, with_answer=False), add_special_tokens=False)["input_ids"],
+              "labels": tokenizer(r["response"], add_special_tokens=False)["input_ids"]} for r in test]
+    return windows, tests

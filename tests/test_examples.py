@@ -219,3 +219,54 @@ def test_bert_tp_dp_example(tmp_path):
     assert torch.isfinite(torch.tensor(torch.load(tmp_path / "bert_loss.pt")))
     m = json.load(open(tmp_path / "results.json"))
     assert {x["MetricName"] for x in m["results"]["metrics"]} >= {"Final loss", "Average throughput"}
+
+
+def _w_finetune(rank, world, hf_dir, data, out_dir, tp):
+    sys.path.insert(0, os.path.join(ROOT, "examples", "training", "llama"))
+    import tp_llama_hf_finetune as ex
+
+    before, after = ex.main(["--hf_model_dir", hf_dir, "--data_file", data, "--output_dir", out_dir,
+                             "--tensor_parallel_size", str(tp), "--seq_len", "64", "--max_steps", "40",
+                             "--lr", "1e-2", "--warmup_steps", "2", "--test_size", "4", "--use_zero_1",
+                             "--sequence_parallel_enabled", "--checkpoint_dir", os.path.join(out_dir, "ckpt")])
+    if rank == 0:
+        torch.save((before, after), os.path.join(out_dir, f"ft_{tp}.pt"))
+
+
+def test_llama_instruction_finetune_example(tmp_path):
+    """examples/training/llama/tp_llama_hf_finetune.py (reference E3 fine-tuning path): HF Llama
+    checkpoint + tokenizer -> TP shard -> packed Dolly-style data -> response loss drops; the
+    pre-training response loss is the same at TP1 and TP2 (HF->NxD conversion + sharding)."""
+    from tokenizers import Tokenizer, models, pre_tokenizers
+    from transformers import LlamaConfig, LlamaForCausalLM, PreTrainedTokenizerFast
+
+    words = ("what is the color of sky grass sun water fire snow answer blue green yellow clear red white "
+             "name a animal that can fly swim run bird fish horse tell me about").split()
+    vocab = {w: i for i, w in enumerate(["<unk>", "<s>", "</s>", "###", "Instruction", "Context", "Answer"]
+                                        + sorted(set(words)))}
+    tk = Tokenizer(models.WordLevel(vocab, unk_token="<unk>"))
+    tk.pre_tokenizer = pre_tokenizers.Whitespace()
+    hf_dir = str(tmp_path / "hf")
+    PreTrainedTokenizerFast(tokenizer_object=tk, unk_token="<unk>", bos_token="<s>", eos_token="</s>"
+                            ).save_pretrained(hf_dir)
+    cfg = LlamaConfig(hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=64, max_position_embeddings=128, rope_theta=10000.0)
+    torch.manual_seed(0)
+    LlamaForCausalLM(cfg).save_pretrained(hf_dir)
+    facts = [("what is the color of sky", "blue"), ("what is the color of grass", "green"),
+             ("what is the color of sun", "yellow"), ("what is the color of snow", "white"),
+             ("what is the color of fire", "red"), ("what is the color of water", "clear"),
+             ("name a animal that can fly", "bird"), ("name a animal that can swim", "fish"),
+             ("name a animal that can run", "horse")]
+    data = str(tmp_path / "data.jsonl")
+    with open(data, "w") as f:
+        for _ in range(6):
+            for q, ans in facts:
+                f.write(json.dumps({"instruction": q, "context": "", "response": ans}) + "\n")
+    run_distributed(_w_finetune, 2, hf_dir, data, str(tmp_path / "tp2"), 2)
+    run_distributed(_w_finetune, 1, hf_dir, data, str(tmp_path / "tp1"), 1)
+    b2, a2 = torch.load(tmp_path / "tp2" / "ft_2.pt")
+    b1, a1 = torch.load(tmp_path / "tp1" / "ft_1.pt")
+    assert abs(b1 - b2) < 1e-4 * max(1.0, abs(b1)), (b1, b2)
+    assert a2 < 0.6 * b2 and a1 < 0.6 * b1, (b1, a1, b2, a2)
+    assert os.path.exists(tmp_path / "tp2" / "ckpt" / "step_40" / "done")
