@@ -3,7 +3,7 @@
 Chunk-interleaved SP layout
 ---------------------------
 Megatron SP gives TP rank r the contiguous rows [r*S/tp, (r+1)*S/tp) of the sequence.  Here the
-sequence is first cut into `c` chunks (NXD_SP_CHUNKS, default 4) and EACH chunk is split over the
+sequence is first cut into `c` chunks (NXD_SP_CHUNKS; default per TP degree, see _DEFAULT_CHUNKS) and EACH chunk is split over the
 TP ranks: the local shard of rank r is [chunk 0 part r | chunk 1 part r | ...].  Everything outside
 the TP regions (residual stream, RMSNorm, dropout) is row-wise, so the row order of a local shard is
 irrelevant to the math — but with this layout the all-gather of chunk j returns the CONTIGUOUS
@@ -34,20 +34,29 @@ from ..ops import gemm as _gemm
 from ..parallel import comm
 from .parallel_state import get_tensor_model_parallel_group
 
-_SP_CHUNKS = int(os.environ.get("NXD_SP_CHUNKS", "4"))
+_SP_CHUNKS = int(os.environ["NXD_SP_CHUNKS"]) if "NXD_SP_CHUNKS" in os.environ else None
+
+# Default chunk count per TP degree.  Chunking trades exposed communication for smaller GEMMs;
+# profiles/r1_sp_chunks_gemm.jsonl (tools/bench_sp_chunks.py) measures the GEMM side per layer
+# (fwd + dgrad, Llama-3-8B, S=8192): TP8 0.74 / 0.83 / 1.13 ms and TP2 2.58 / 2.57 / 2.99 ms for
+# c = 1 / 2 / 4.  With a ring collective of time T per op the exposed part is ~max(T + g/c,
+# T/c + g) - g; over the plausible xGMI range (T = 70-300 us at TP8) c=2 beats c=4 at TP8 by
+# >= 120 us per layer, while TP2 (one link pair, T ~ 440 us) still prefers c=4.
+_DEFAULT_CHUNKS = {2: 4, 4: 2, 8: 2}
 
 
-def set_sequence_parallel_chunks(c: int) -> None:
+def set_sequence_parallel_chunks(c: Optional[int]) -> None:
+    """Override the chunk count for every TP degree (None restores the per-degree defaults)."""
     global _SP_CHUNKS
-    _SP_CHUNKS = max(1, int(c))
+    _SP_CHUNKS = None if c is None else max(1, int(c))
 
 
-def get_sequence_parallel_chunks() -> int:
-    return _SP_CHUNKS
+def get_sequence_parallel_chunks(tp: int = 8) -> int:
+    return _SP_CHUNKS if _SP_CHUNKS is not None else _DEFAULT_CHUNKS.get(tp, 2)
 
 
-def _chunks(local_rows: int) -> int:
-    c = _SP_CHUNKS
+def _chunks(local_rows: int, tp: int = 8) -> int:
+    c = get_sequence_parallel_chunks(tp)
     while c > 1 and local_rows % c:
         c -= 1
     return c
@@ -65,7 +74,7 @@ def gather_start(x: torch.Tensor, group=None) -> Tuple[torch.Tensor, List, int]:
     tp = _ws(group)
     x = x.contiguous()
     Sl = x.shape[0]
-    c = _chunks(Sl)
+    c = _chunks(Sl, tp)
     full = torch.empty((tp * Sl,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     fv = full.view((c, tp * (Sl // c)) + tuple(x.shape[1:]))
     xv = x.view((c, Sl // c) + tuple(x.shape[1:]))
@@ -93,7 +102,7 @@ def sp_reduce_scatter(x: torch.Tensor, group=None) -> torch.Tensor:
     S = x.shape[0]
     assert S % tp == 0, f"sequence {S} not divisible by TP {tp}"
     Sl = S // tp
-    c = _chunks(Sl)
+    c = _chunks(Sl, tp)
     out = torch.empty((Sl,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     ov = out.view((c, Sl // c) + tuple(x.shape[1:]))
     xv = x.view((c, S // c) + tuple(x.shape[1:]))
@@ -112,7 +121,7 @@ def sp_split(x: torch.Tensor, group=None) -> torch.Tensor:
     r = dist.get_rank(group=group)
     S = x.shape[0]
     Sl = S // tp
-    c = _chunks(Sl)
+    c = _chunks(Sl, tp)
     return x.reshape((c, tp, Sl // c) + tuple(x.shape[1:]))[:, r].reshape((Sl,) + tuple(x.shape[1:])).contiguous()
 
 
@@ -151,7 +160,7 @@ def _gemm_reduce_scatter(fn, x_full: torch.Tensor, n_out: int, group) -> Tuple[t
     tp = _ws(group)
     S = x_full.shape[0]
     Sl = S // tp
-    c = _chunks(Sl)
+    c = _chunks(Sl, tp)
     out_full = torch.empty(tuple(x_full.shape[:-1]) + (n_out,), dtype=x_full.dtype, device=x_full.device)
     local = torch.empty((Sl,) + tuple(out_full.shape[1:]), dtype=x_full.dtype, device=x_full.device)
     xv = x_full.view((c, S // c) + tuple(x_full.shape[1:]))
