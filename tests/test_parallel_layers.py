@@ -152,11 +152,11 @@ def test_gqa_qkv(mult):
     run_distributed(_w_qkv, 2, mult)
 
 
-def _w_tiny_llama(rank, world, sp):
+def _w_tiny_llama(rank, world, sp, over=None):
     from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
 
     ps.initialize_model_parallel(world)
-    cfg = llama_config("tiny", sequence_parallel_enabled=sp)
+    cfg = llama_config("tiny", sequence_parallel_enabled=sp, **(over or {}))
     torch.manual_seed(0)
     model = LlamaForCausalLM(cfg, dtype=torch.float32)
     torch.manual_seed(5)
@@ -172,7 +172,7 @@ def _w_tiny_llama(rank, world, sp):
         for t in parts:
             dist.all_reduce(t)
         dup = torch.stack([t.norm() ** 2 for t in parts]).sum()
-    torch.save({"loss": loss.detach(), "gn": (gn + dup).detach()}, f"/tmp/nxd_tiny_llama_{world}_{sp}_{rank}.pt")
+    torch.save({"loss": loss.detach(), "gn": (gn + dup).detach()}, f"/tmp/nxd_tiny_llama_{world}_{sp}_{rank}{'_h8' if over else ''}.pt")
 
 
 @pytest.mark.parametrize("sp", [False, True])
@@ -184,3 +184,14 @@ def test_tiny_llama_tp2_matches_tp1(sp):
     r2 = torch.load(f"/tmp/nxd_tiny_llama_2_{sp}_0.pt")
     torch.testing.assert_close(r1["loss"], r2["loss"], atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(r1["gn"], r2["gn"], atol=1e-3, rtol=1e-3)
+
+
+def test_tiny_llama_tp4_sp_matches_tp1():
+    """TP=4 with sequence parallelism (default 2 SP chunks at TP4, vs 4 at TP2) == TP=1."""
+    over = {"num_attention_heads": 8, "num_key_value_heads": 4}
+    run_distributed(_w_tiny_llama, 1, False, over)
+    run_distributed(_w_tiny_llama, 4, True, over)
+    r1 = torch.load("/tmp/nxd_tiny_llama_1_False_0_h8.pt")
+    r4 = torch.load("/tmp/nxd_tiny_llama_4_True_0_h8.pt")
+    torch.testing.assert_close(r1["loss"], r4["loss"], atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(r1["gn"], r4["gn"], atol=1e-3, rtol=1e-3)
