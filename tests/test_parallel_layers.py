@@ -152,6 +152,10 @@ def test_gqa_qkv(mult):
     run_distributed(_w_qkv, 2, mult)
 
 
+def _tag(over):
+    return f"_h{over['num_attention_heads']}kv{over['num_key_value_heads']}" if over else ""
+
+
 def _w_tiny_llama(rank, world, sp, over=None):
     from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
 
@@ -172,7 +176,7 @@ def _w_tiny_llama(rank, world, sp, over=None):
         for t in parts:
             dist.all_reduce(t)
         dup = torch.stack([t.norm() ** 2 for t in parts]).sum()
-    torch.save({"loss": loss.detach(), "gn": (gn + dup).detach()}, f"/tmp/nxd_tiny_llama_{world}_{sp}_{rank}{'_h8' if over else ''}.pt")
+    torch.save({"loss": loss.detach(), "gn": (gn + dup).detach()}, f"/tmp/nxd_tiny_llama_{world}_{sp}_{rank}{_tag(over)}.pt")
 
 
 @pytest.mark.parametrize("sp", [False, True])
@@ -191,7 +195,18 @@ def test_tiny_llama_tp4_sp_matches_tp1():
     over = {"num_attention_heads": 8, "num_key_value_heads": 4}
     run_distributed(_w_tiny_llama, 1, False, over)
     run_distributed(_w_tiny_llama, 4, True, over)
-    r1 = torch.load("/tmp/nxd_tiny_llama_1_False_0_h8.pt")
-    r4 = torch.load("/tmp/nxd_tiny_llama_4_True_0_h8.pt")
+    r1 = torch.load(f"/tmp/nxd_tiny_llama_1_False_0{_tag(over)}.pt")
+    r4 = torch.load(f"/tmp/nxd_tiny_llama_4_True_0{_tag(over)}.pt")
     torch.testing.assert_close(r1["loss"], r4["loss"], atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(r1["gn"], r4["gn"], atol=1e-3, rtol=1e-3)
+
+
+def test_tiny_llama_tp8_sp_matches_tp1():
+    """The headline layout in miniature: TP=8 + SP (1 kv head per rank, 2 SP chunks) == TP=1."""
+    over = {"num_attention_heads": 8, "num_key_value_heads": 8}
+    run_distributed(_w_tiny_llama, 1, False, over)
+    run_distributed(_w_tiny_llama, 8, True, over)
+    r1 = torch.load(f"/tmp/nxd_tiny_llama_1_False_0{_tag(over)}.pt")
+    r8 = torch.load(f"/tmp/nxd_tiny_llama_8_True_0{_tag(over)}.pt")
+    torch.testing.assert_close(r1["loss"], r8["loss"], atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(r1["gn"], r8["gn"], atol=1e-3, rtol=1e-3)
