@@ -270,9 +270,9 @@ def load_checkpoint(path: str, tag: Optional[str] = None, model=None, optimizer=
         optimizer.load_state_dict(osd)
     if scheduler is not None and storage.file_exists(os.path.join(tag, "scheduler.pt")):
         scheduler.load_state_dict(storage.load_object(os.path.join(tag, "scheduler.pt"), map_location="cpu",
-                                                      weights_only=False))
+                                                      weights_only=weights_only))
     user = None
     if storage.file_exists(os.path.join(tag, "user_content.pt")):
-        user = storage.load_object(os.path.join(tag, "user_content.pt"), map_location="cpu", weights_only=False)
+        user = storage.load_object(os.path.join(tag, "user_content.pt"), map_location="cpu", weights_only=weights_only)
     _barrier()
     return user
