@@ -9,6 +9,9 @@ global batch.  `--parallelism dp` instead runs TP=1 x DP=N (weak scaling).
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+Without a launcher (no WORLD_SIZE in the environment) and N > 1, bench.py starts the N rank
+processes itself (child processes, before any HIP call) and waits for them.
+
 Times exactly K optimizer steps between barrier + device synchronisation on both sides, takes
 the max over ranks, rank 0 prints one JSON line.
 """
@@ -18,20 +21,13 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config  # noqa: E402
-from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW  # noqa: E402
-from neuronx_distributed_llama3_2_amd.parallel.grad_buffer import find_shared_params  # noqa: E402
-from neuronx_distributed_llama3_2_amd.parallel_layers import parallel_state as ps  # noqa: E402
-from neuronx_distributed_llama3_2_amd.parallel_layers.random import model_parallel_manual_seed  # noqa: E402
-from neuronx_distributed_llama3_2_amd.utils.profiling import llama_num_params, mfu, model_flops_per_token  # noqa: E402
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
 
 BASELINE_TOKENS_PER_S = None  # the reference publishes no Llama-3-8B throughput
 
@@ -49,27 +45,86 @@ def parse():
     ap.add_argument("--layers", type=int, default=None, help="override #layers (NOT the headline config)")
     ap.add_argument("--no-sp", action="store_true")
     ap.add_argument("--ckpt", default=None, help="activation checkpointing: None | full | selective")
+    ap.add_argument("--cpu", action="store_true", help="force the CPU/gloo path (plumbing tests)")
     return ap.parse_args()
 
 
-def main():
-    a = parse()
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_local_ranks(argv, n: int) -> int:
+    """`python bench.py --gpus N` without a launcher: start N fresh rank processes (one per GPU,
+    RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set) and wait for them.  The parent never imports torch or
+    touches the GPU and never execs; if one rank fails the others are terminated and the parent
+    exits non-zero with the first failing rank's code."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def main(a):
+    import torch
+    import torch.distributed as dist
+
+    from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
+    from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW
+    from neuronx_distributed_llama3_2_amd.parallel.grad_buffer import find_shared_params
+    from neuronx_distributed_llama3_2_amd.parallel_layers import parallel_state as ps
+    from neuronx_distributed_llama3_2_amd.parallel_layers.random import model_parallel_manual_seed
+    from neuronx_distributed_llama3_2_amd.utils.profiling import llama_num_params, mfu, model_flops_per_token
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    assert world == a.gpus, f"--gpus {a.gpus} but WORLD_SIZE={world}"
-    use_cuda = torch.cuda.is_available()
+    if world != a.gpus:
+        raise SystemExit(f"bench: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    use_cuda = torch.cuda.is_available() and not a.cpu
     if use_cuda:
+        ndev = torch.cuda.device_count()
+        if local_rank >= ndev:
+            raise SystemExit(f"bench: LOCAL_RANK {local_rank} but only {ndev} visible GPUs")
         torch.cuda.set_device(local_rank)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
-    dist.init_process_group("nccl" if use_cuda else "gloo", rank=rank, world_size=world,
+    if not use_cuda:
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // world))
+    backend = "nccl" if use_cuda else "gloo"
+    dist.init_process_group(backend, rank=rank, world_size=world,
                             device_id=torch.device("cuda", local_rank) if use_cuda else None)
+    dev = torch.device("cuda", local_rank) if use_cuda else torch.device("cpu")
+    # preflight: one all-reduce over the whole job must see every rank (RCCL on GPU)
+    probe = torch.ones(1, device=dev)
+    dist.all_reduce(probe)
+    comm_world = int(probe.item())
+    if comm_world != world:
+        raise SystemExit(f"bench: {backend} all-reduce saw {comm_world} ranks, expected {world}")
+
     tp = min(world, 8) if a.parallelism == "tp" else 1
     ps.initialize_model_parallel(tensor_model_parallel_size=tp)
     dp = ps.get_data_parallel_size()
     model_parallel_manual_seed(1234)
-    dev = torch.device("cuda", local_rank) if use_cuda else torch.device("cpu")
 
     over = dict(sequence_parallel_enabled=(tp > 1 and not a.no_sp), max_position_embeddings=max(8192, a.seq))
     if a.layers is not None:
@@ -87,15 +142,22 @@ def main():
     opt = FlatMixedPrecisionAdamW([{"params": decay, "weight_decay": 0.01}, {"params": no_decay, "weight_decay": 0.0}],
                                   lr=1e-5, betas=(0.9, 0.95), eps=1e-8, zero1=dp > 1, grad_clipping=True,
                                   max_grad_norm=1.0, shared_param_ids=find_shared_params(model))
-    assert a.gbs % (a.mbs * dp) == 0, "global batch must be divisible by micro-batch x DP"
+    if a.gbs % (a.mbs * dp):
+        raise SystemExit(f"bench: global batch {a.gbs} not divisible by micro-batch {a.mbs} x DP {dp}")
     accum = a.gbs // (a.mbs * dp)
+    # a fresh batch for every micro-step of every step (warmup included), generated before the timed
+    # region; identical across the TP ranks of one DP rank, different across DP ranks.  Random tokens
+    # cannot be memorised, so the reported loss stays near ln(V) and flags numerics regressions.
     g = torch.Generator(device="cpu").manual_seed(4321 + ps.get_data_parallel_rank())
-    batches = [torch.randint(0, cfg.vocab_size, (a.mbs, a.seq), generator=g).to(dev) for _ in range(min(accum, 4))]
+    n_micro = accum * (a.warmup + a.steps)
+    batches = torch.randint(0, cfg.vocab_size, (n_micro, a.mbs, a.seq), generator=g).to(dev)
+    cursor = [0]
 
     def train_step():
         for i in range(accum):
             opt.set_grad_sync(i == accum - 1)
-            ids = batches[i % len(batches)]
+            ids = batches[cursor[0]]
+            cursor[0] += 1
             out = model(ids, labels=ids)
             (out.loss / accum).backward()
         opt.step()
@@ -135,12 +197,14 @@ def main():
             "scaling": "strong" if a.parallelism == "tp" else "weak",
             "vs_baseline": (value / BASELINE_TOKENS_PER_S) if BASELINE_TOKENS_PER_S else None,
             "dtype": "bf16",
-            "data": "synthetic (random token ids, random-init weights)",
+            "data": "synthetic (fresh random token ids per micro-step, random-init weights)",
             "config": {"model": a.model if a.layers is None else f"{a.model}-{a.layers}L", "global_batch": a.gbs,
                        "micro_batch": a.mbs, "seq_len": a.seq, "parallelism": par, "grad_accum": accum,
                        "optimizer": "AdamW fp32-master" + (" ZeRO-1" if dp > 1 else ""),
                        "activation_checkpoint": a.ckpt or "none"},
             "loss": round(float(loss.item()), 4),
+            "comm_backend": backend,
+            "comm_world_size": comm_world,
             "params_per_rank": nparams_local,
             "model_params": nparams,
             "mfu": round(mfu(value, fpt, world), 4),   # vs 2.5 PFLOP/s dense bf16 per GPU
@@ -152,4 +216,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_local_ranks(sys.argv[1:], args.gpus))
+    main(args)

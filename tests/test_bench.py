@@ -1,0 +1,65 @@
+"""bench.py contract on CPU/gloo: `python bench.py --gpus N` spawns its own N ranks (no launcher),
+the torch.distributed.run form still works, and rank 0 prints exactly one well-formed JSON line."""
+
+import json
+import math
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--model", "tiny", "--seq", "128", "--gbs", "4", "--steps", "1", "--warmup", "1", "--cpu"]
+
+
+def _env():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def _check(rec, n):
+    assert rec["n_gpus"] == n and rec["comm_world_size"] == n
+    assert rec["steps"] == 1 and rec["warmup"] == 1
+    assert rec["config"]["parallelism"] == (f"tp{n}_sp" if n > 1 else "tp1")
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0
+    # fresh random tokens every micro-step: loss stays near ln(V) (no memorisation)
+    assert abs(rec["loss"] - math.log(1024)) < 0.5, rec["loss"]
+    for k in ("metric", "unit", "higher_is_better", "scaling", "vs_baseline", "dtype", "data"):
+        assert k in rec
+
+
+@pytest.mark.parametrize("n", [1, 4])
+def test_bench_self_spawn(n):
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), *ARGS], cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    _check(recs[0], n)
+
+
+def test_bench_torchrun():
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29631", "bench.py", "--gpus", "2", *ARGS],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    _check(recs[0], 2)
+
+
+def test_bench_rank_failure_propagates():
+    # a launcher whose world size disagrees with --gpus must fail loudly, not hang
+    env = _env()
+    env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_PORT="29632")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", *ARGS], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in (r.stderr + r.stdout)
