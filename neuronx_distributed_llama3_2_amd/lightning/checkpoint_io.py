@@ -19,7 +19,7 @@ def _shard_name() -> str:
 
 
 class NeuronCheckpointIO(CheckpointIO):
-    def __init__(self, save_load_xser: bool = True, weights_only: bool = False, *args, **kwargs):
+    def __init__(self, save_load_xser: bool = True, weights_only: bool = True, *args, **kwargs):
         super().__init__(*args, **kwargs)
         self.save_load_xser = save_load_xser
         self.weights_only = weights_only

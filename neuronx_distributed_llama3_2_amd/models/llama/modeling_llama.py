@@ -197,6 +197,7 @@ class LlamaForCausalLM(nn.Module):
         if getattr(config, "tie_word_embeddings", False):
             assert self.lm_head.weight.shape == self.model.embed_tokens.weight.shape
             self.lm_head.weight = self.model.embed_tokens.weight
+            self.lm_head.weight._nxd_tied = True   # grad buffers defer this bucket's reduction
 
     def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                 labels: Optional[torch.Tensor] = None, position_ids=None, **unused) -> CausalLMOutput:

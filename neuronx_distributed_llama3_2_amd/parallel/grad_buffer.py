@@ -122,7 +122,8 @@ class FlatBuffer:
         self.offsets = offsets
         # pipeline-shared parameters (tied across stages) are summed across stages at the end of the
         # step, so their bucket must wait for the final synchronisation too
-        self.buckets = [_Bucket(s, e, ps, any(id(q) in shared_ids or getattr(q, "_nxd_pp_shared", False) for q in ps))
+        self.buckets = [_Bucket(s, e, ps, any(id(q) in shared_ids or getattr(q, "_nxd_pp_shared", False)
+                                                  or getattr(q, "_nxd_tied", False) for q in ps))
                         for (s, e, ps) in buckets_spec]
         self._bucket_of = {id(p): b for b in self.buckets for p in b.params}
         # Overlap is ARMED per step: the training loop (or the pipeline runtime) calls set_sync(True)
@@ -244,3 +245,15 @@ def find_shared_params(model: torch.nn.Module) -> set:
         for _, p in m.named_parameters(recurse=False):
             count[id(p)] += 1
     return {k for k, v in count.items() if v > 1}
+
+
+def tag_shared_params(model: torch.nn.Module) -> set:
+    """Mark parameters registered in more than one module (tied embeddings) with `_nxd_tied` so
+    every FlatBuffer built over them later -- whatever optimizer front-end builds it and whether or
+    not it is handed the model -- defers their bucket's reduction to `finish_grad_sync` (the second
+    use's gradient lands after the first use's hook fired)."""
+    ids = find_shared_params(model)
+    for p in model.parameters():
+        if id(p) in ids:
+            p._nxd_tied = True
+    return ids

@@ -26,6 +26,7 @@ import torch.distributed as dist
 
 from ..parallel_layers.parallel_state import (
     get_data_parallel_rank,
+    get_expert_data_parallel_rank,
     get_expert_model_parallel_rank,
     get_expert_model_parallel_size,
     get_pipeline_model_parallel_rank,
@@ -215,7 +216,10 @@ def save_checkpoint(checkpoint_dir_str: str, tag: str, model=None, optimizer=Non
     dpr, _, _, _ = _ranks()
     ep = model_parallel_is_initialized() and get_expert_model_parallel_size() > 1
     if model is not None:
-        if dpr == 0 or ep:
+        # one writer per distinct model shard: DP rank 0, or with EP the expert-data-parallel rank 0
+        # of every EP rank (EDP replicas hold identical shards and would race on one path;
+        # reference trainer/checkpoint.py:496)
+        if (get_expert_data_parallel_rank() == 0) if ep else (dpr == 0):
             st.add_save_task(_model_state(model), os.path.join(str(tag), _get_path("model", ep=ep)), xser=use_xser)
     if optimizer is not None:
         zero = zero1_optimizer or _is_zero1(optimizer)

@@ -58,8 +58,10 @@ class FilesysCheckpointStorage(BaseCheckpointStorage):
     def list_checkpoint_tags(self) -> List[str]:
         if not os.path.isdir(self._dirname):
             return []
-        tags = [d for d in os.listdir(self._dirname) if os.path.isdir(self._p(d))]
-        tags.sort(key=lambda d: os.path.getmtime(self._p(d)))
+        # only directories carrying the `checkpoint` begin marker are tags: anything else a user
+        # keeps under the checkpoint dir (logs, tensorboard, outputs) is never listed, so never GC'd
+        tags = [d for d in os.listdir(self._dirname) if os.path.isfile(self._p(os.path.join(d, "checkpoint")))]
+        tags.sort(key=lambda d: os.path.getmtime(self._p(os.path.join(d, "checkpoint"))))
         return tags
 
     def file_exists(self, filename: str) -> bool:
@@ -87,7 +89,7 @@ class FilesysCheckpointStorage(BaseCheckpointStorage):
     def save_object(self, obj: Any, filename: str) -> None:
         path = self._p(filename)
         os.makedirs(os.path.dirname(path), exist_ok=True)
-        tmp = path + ".tmp"
+        tmp = f"{path}.tmp.{os.getpid()}"   # unique per writer: concurrent writers never share a tmp
         torch.save(obj, tmp)
         os.replace(tmp, path)
 
@@ -139,7 +141,15 @@ class S3CheckpointStorage(BaseCheckpointStorage):
 
     def list_checkpoint_tags(self) -> List[str]:  # pragma: no cover - network
         resp = self._retry(self.client.list_objects_v2, Bucket=self.bucket, Prefix=self._key(""), Delimiter="/")
-        return [p["Prefix"].rstrip("/").split("/")[-1] for p in resp.get("CommonPrefixes", [])]
+        tags = []
+        for p in resp.get("CommonPrefixes", []):
+            tag = p["Prefix"].rstrip("/").split("/")[-1]
+            try:
+                head = self._retry(self.client.head_object, Bucket=self.bucket, Key=self._key(f"{tag}/checkpoint"))
+            except Exception:
+                continue   # no begin marker: not a checkpoint tag
+            tags.append((head["LastModified"], tag))
+        return [t for _, t in sorted(tags)]
 
     def file_exists(self, filename: str) -> bool:  # pragma: no cover - network
         try:

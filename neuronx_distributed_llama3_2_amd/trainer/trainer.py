@@ -124,6 +124,9 @@ def initialize_parallel_model(nxd_config: Dict[str, Any], model_fn, *model_args,
     if nxd_config["pad_model"]:
         assert is_hf_pretrained_model(base_model) or hasattr(base_model, "config"), "pad_model needs a model config"
         model = pad_model(model, parallel_state.get_tensor_model_parallel_size(), base_model.config.num_attention_heads)
+    from ..parallel.grad_buffer import tag_shared_params
+
+    tag_shared_params(model)
     nxd_model = NxDModel(model, nxd_config)
     ac = nxd_config["activation_checkpoint_config"]
     if ac is not None:
@@ -156,7 +159,12 @@ def initialize_optimizer_from_class(nxd_config, optimizer_class, parameters, mod
         from ..optimizer.zero_redundancy_optimizer import NeuronEPZero1Optimizer, NeuronZero1Optimizer
 
         cls = NeuronEPZero1Optimizer if parallel_state.get_expert_model_parallel_size() > 1 else NeuronZero1Optimizer
-        return cls(parameters, optimizer_class, grad_clipping=ocfg["grad_clipping"],
+        shared = None
+        if model is not None:
+            from ..parallel.grad_buffer import tag_shared_params
+
+            shared = tag_shared_params(model)
+        return cls(parameters, optimizer_class, grad_clipping=ocfg["grad_clipping"], shared_param_ids=shared,
                    max_norm=ocfg.get("max_grad_norm", 1.0),
                    save_master_weights=mp.get("use_master_weights_in_ckpt", False), **defaults)
     if mp.get("use_fp32_grad_acc", False) or mp.get("use_master_weights_in_ckpt", False):

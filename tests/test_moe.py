@@ -192,3 +192,54 @@ def test_mixtral_trains_tp_ep():
     assert a[-1] < a[0] and b[-1] < b[0] and c[-1] < c[0], (a, b, c)
     for x, y in zip(a, b):
         assert abs(x - y) < 2e-3 * abs(x), (a, b)
+
+
+def _w_mixtral_ckpt(rank, world, ep, ckpt_dir, resume, out):
+    import neuronx_distributed_llama3_2_amd as nxd
+    from neuronx_distributed_llama3_2_amd.models.mixtral import MixtralForCausalLM, mixtral_config
+
+    cfg_nxd = nxd.neuronx_distributed_config(tensor_parallel_size=1, expert_parallel_size=ep,
+                                            optimizer_config={"zero_one_enabled": True, "grad_clipping": True,
+                                                              "max_grad_norm": 1.0})
+    cfg = mixtral_config("tiny", capacity_factor=2.0)
+    torch.manual_seed(0)
+    model = nxd.initialize_parallel_model(cfg_nxd, MixtralForCausalLM, cfg, torch.float32)
+    opt = nxd.initialize_parallel_optimizer(cfg_nxd, torch.optim.AdamW, model.parameters(), lr=3e-3)
+    g = torch.Generator().manual_seed(3)
+    batches = [torch.randint(0, cfg.vocab_size, (4, 32), generator=g) for _ in range(6)]
+    dp, dpr = ps.get_data_parallel_size(), ps.get_data_parallel_rank()
+    start = 0
+    if resume:
+        start = nxd.load_checkpoint(ckpt_dir, model=model, optimizer=opt)["step"]
+    losses = []
+    for step in range(start, 6):
+        local = batches[step].chunk(dp)[dpr]
+        o = model(local, labels=local)
+        o.loss.backward()
+        opt.step()
+        opt.zero_grad()
+        l = o.loss.detach().clone()
+        torch.distributed.all_reduce(l)
+        losses.append(float(l) / world)
+        if not resume and step == 2:
+            nxd.save_checkpoint(ckpt_dir, "step_3", model=model, optimizer=opt, user_content={"step": 3})
+    nxd.finalize_checkpoint()
+    if rank == 0:
+        torch.save(losses, out)
+
+
+def test_mixtral_ep2_edp2_checkpoint_resume():
+    """EP=2 x expert-data-parallel 2 (4 ranks): one writer per EP shard (no EDP race on the model
+    file), and resuming from step 3 reproduces the uninterrupted run."""
+    d = tempfile.mkdtemp()
+    ck = os.path.join(d, "ck")
+    run_distributed(_w_mixtral_ckpt, 4, 2, ck, False, os.path.join(d, "full.pt"))
+    files = sorted(os.listdir(os.path.join(ck, "step_3", "model")))
+    assert files == ["dp_rank_00_ep_rank_00_tp_rank_00_pp_rank_00.pt",
+                     "dp_rank_00_ep_rank_01_tp_rank_00_pp_rank_00.pt"], files
+    assert not [f for f in os.listdir(os.path.join(ck, "step_3", "optim")) if ".tmp" in f]
+    run_distributed(_w_mixtral_ckpt, 4, 2, ck, True, os.path.join(d, "res.pt"))
+    full, res = torch.load(os.path.join(d, "full.pt")), torch.load(os.path.join(d, "res.pt"))
+    assert len(res) == 3
+    for x, y in zip(full[3:], res):
+        assert abs(x - y) < 1e-5, (full, res)
