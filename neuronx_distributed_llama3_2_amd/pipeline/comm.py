@@ -18,11 +18,23 @@ from ..parallel_layers import parallel_state as ps
 
 
 class P2PGroup:
-    """Collects p2p ops, then issues them as one group and waits."""
+    """Asynchronous p2p runtime of one pipeline step.
+
+    `send`/`recv` collect ops; `issue()` submits everything collected since the previous issue as
+    ONE `batch_isend_irecv` exchange (neighbours' exchanges pair up in issue order, which is what
+    keeps bidirectional traffic deadlock-free) and returns immediately: on RCCL the transfer runs
+    on the communicator's own HIP stream while the compute stream keeps going.  Only a consumer
+    waits -- `wait_for(tensors)` waits the exchange(s) that fill those receive buffers (on RCCL a
+    stream-level wait: the host never blocks) -- and sent buffers stay referenced until their
+    exchange is retired, so a send never blocks the next compute task.  `flush()` retires all.
+    """
 
     def __init__(self):
         self.ops: List[dist.P2POp] = []
         self.keep: List[torch.Tensor] = []
+        self._inflight: List[Tuple[list, List[torch.Tensor]]] = []   # (works, tensors) per exchange
+        self._exchange_of: dict = {}                                  # id(recv buffer) -> exchange
+        self.max_inflight = 64   # bound on outstanding exchanges (oldest retired first)
 
     def send(self, t: torch.Tensor, dst: int):
         t = t.contiguous()
@@ -30,16 +42,47 @@ class P2PGroup:
         self.ops.append(dist.P2POp(dist.isend, t, dst))
 
     def recv(self, t: torch.Tensor, src: int):
+        self.keep.append(t)
         self.ops.append(dist.P2POp(dist.irecv, t, src))
 
-    def flush(self):
+    def issue(self) -> None:
         if not self.ops:
             return
-        reqs = dist.batch_isend_irecv(self.ops)
-        for r in reqs:
-            r.wait()
-        self.ops = []
-        self.keep = []
+        works = dist.batch_isend_irecv(self.ops)
+        ex = (list(works), self.keep)
+        self._inflight.append(ex)
+        for op in self.ops:
+            if op.op is dist.irecv:
+                self._exchange_of[id(op.tensor)] = ex
+        self.ops, self.keep = [], []
+        while len(self._inflight) > self.max_inflight:
+            self._retire(self._inflight[0])
+
+    def _retire(self, ex) -> None:
+        works, tensors = ex
+        for w in works:
+            w.wait()
+        works.clear()
+        for t in tensors:
+            self._exchange_of.pop(id(t), None)
+        if ex in self._inflight:
+            self._inflight.remove(ex)
+
+    def wait_for(self, tensors) -> None:
+        """Make the receive buffers in `tensors` safe to read (issues pending ops first)."""
+        self.issue()
+        for t in tensors:
+            ex = self._exchange_of.get(id(t))
+            if ex is not None:
+                self._retire(ex)
+
+    def pending(self) -> int:
+        return len(self._inflight) + (1 if self.ops else 0)
+
+    def flush(self):
+        self.issue()
+        while self._inflight:
+            self._retire(self._inflight[0])
 
 
 def send(tensor: torch.Tensor, dst: int) -> None:

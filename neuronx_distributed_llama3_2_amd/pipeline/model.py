@@ -59,6 +59,19 @@ from .trace import trace_model
 logger = get_logger()
 
 
+def _record_saved(saved: set):
+    def pack(t):
+        if isinstance(t, torch.Tensor) and t.device.type != "meta":
+            saved.add(t.untyped_storage().data_ptr())
+        return t
+
+    return pack
+
+
+def _identity(t):
+    return t
+
+
 class NxDPPModel(nn.Module):
     def __init__(self, module: nn.Module, transformer_layer_cls=None, num_microbatches: int = 1,
                  virtual_pipeline_size: int = 1, output_loss_value_spec=None, return_mb_loss: bool = False,
@@ -83,6 +96,14 @@ class NxDPPModel(nn.Module):
         self.broadcast_and_average_loss = broadcast_and_average_loss
         self.return_loss_on_cpu = return_loss_on_cpu
         self.deallocate_pipeline_outputs = deallocate_pipeline_outputs
+        # fuse_microbatches (reference :230-233): there the whole step becomes one XLA graph.  Here
+        # the step never blocks the host between micro-batches anyway (async p2p, device losses);
+        # the flag keeps the reference's contract that the loss stays on the device.
+        self.fuse_microbatches = fuse_microbatches
+        if fuse_microbatches and return_loss_on_cpu:
+            logger.warning("return_loss_on_cpu will be set to False when fuse_microbatches is set to True.")
+            self.return_loss_on_cpu = False
+        self.stats: Dict[str, int] = {}
         self.param_init_fn = param_init_fn
         self.input_names = input_names
         if _debug_mode:
@@ -374,8 +395,14 @@ class NxDPPModel(nn.Module):
         def stage_of(task):
             return task.model_chunk * PP + self.pp_rank
 
+        dealloc = train and self.deallocate_pipeline_outputs
+        saved_storages: Dict[Tuple[int, int], set] = {}
+        self.stats = {"held_output_bytes": 0, "held_output_bytes_peak": 0, "deallocated_outputs": 0}
+
         for task in tasks:
-            if isinstance(task, (ForwardStepTask, BackwardStepTask, ReduceGradsTask)):
+            if isinstance(task, (ForwardStepTask, BackwardStepTask)):
+                group.issue()          # exchanges go out; nobody waits for a send
+            elif isinstance(task, ReduceGradsTask):
                 group.flush()
             if isinstance(task, ForwardPreprocessTask):
                 s = stage_of(task)
@@ -392,12 +419,19 @@ class NxDPPModel(nn.Module):
                 label = f"mb_{task.mb}_stage{s}_ForwardStep"
                 self.timeline.mark_event_start(label)
                 env = envs[(task.mb, s)]
-                for name, t in recv_leaves.get((task.mb, s), {}).items():
+                leaves_in = recv_leaves.get((task.mb, s), {})
+                group.wait_for(leaves_in.values())   # only this task's inputs are waited for
+                for name, t in leaves_in.items():
                     if train and t.is_floating_point():
                         t.requires_grad_(True)
                     env[name] = t
                 with torch.set_grad_enabled(train):
-                    self._run_stage(s, env, mbs[task.mb])
+                    if dealloc and s != last_stage:
+                        saved = saved_storages[(task.mb, s)] = set()
+                        with torch.autograd.graph.saved_tensors_hooks(_record_saved(saved), _identity):
+                            self._run_stage(s, env, mbs[task.mb])
+                    else:
+                        self._run_stage(s, env, mbs[task.mb])
                 if s == last_stage:
                     out = self._final_output(env)
                     loss = self._loss_from_output(out)
@@ -411,6 +445,9 @@ class NxDPPModel(nn.Module):
                 env = envs[(task.mb, s)]
                 for name, _, _, _ in self._meta[s]:
                     group.send(env[name].detach(), self._owner(s + 1))
+                if train:
+                    self._account_outputs(env, recv_leaves.get((task.mb, s), {}), s,
+                                          saved_storages.pop((task.mb, s), None) if dealloc else None)
             elif isinstance(task, BackwardPreprocessTask):
                 s = stage_of(task)
                 if s == last_stage:
@@ -436,6 +473,7 @@ class NxDPPModel(nn.Module):
                     (losses_mb * scale).backward()
                 else:
                     gin = grads_in.pop((task.mb, s), {})
+                    group.wait_for(gin.values())
                     outs, grads = [], []
                     for name, g in gin.items():
                         t = env[name]
@@ -446,7 +484,14 @@ class NxDPPModel(nn.Module):
                             outs.append(t)
                             grads.append(g)
                     if outs:
-                        torch.autograd.backward(outs, grads)
+                        if any(getattr(t, "_nxd_dealloc_shape", None) is not None for t in outs):
+                            # deallocated outputs: the C++ engine checks grads against the grad_fn's
+                            # recorded input metadata, not the (now 1-element) tensor
+                            torch.autograd.Variable._execution_engine.run_backward(
+                                tuple(outs), tuple(grads), False, False, tuple(), True, True)
+                        else:
+                            torch.autograd.backward(outs, grads)
+                    self._release_outputs(env, s)
                 envs.pop((task.mb, s), None)
                 self.timeline.mark_event_end(label)
             elif isinstance(task, BackwardPostprocessTask):
@@ -463,6 +508,40 @@ class NxDPPModel(nn.Module):
                 self._reduce_shared_grads()
         group.flush()
         return losses, outputs
+
+    def _account_outputs(self, env, leaves, s, saved) -> None:
+        """After a stage's outputs were handed to the p2p runtime: track the activation bytes the
+        stage keeps for backward and, with `deallocate_pipeline_outputs`, pseudo-free every output
+        whose values backward does not need (reference pipeline/model.py:921-939): its storage is
+        swapped for one element and only the autograd node is kept.  Unlike the reference, an
+        output is freed only if no autograd node saved it (recorded by a saved-tensor hook during
+        the stage forward), so it is safe for any stage boundary, e.g. a fused residual-add whose
+        sum the norm backward re-reads."""
+        held = 0
+        for name, _, _, _ in self._meta[s]:
+            t = env[name]
+            if not isinstance(t, torch.Tensor) or (name in leaves and t is leaves[name]):
+                continue
+            base = t._base
+            free = (saved is not None and t.requires_grad and t.numel() > 1
+                    and t.untyped_storage().data_ptr() not in saved
+                    # a whole-tensor alias (e.g. an identity TP mapping at TP=1) frees its base too
+                    and (base is None or (base.numel() == t.numel() and base._base is None)))
+            if free:
+                t._nxd_dealloc_shape = t.shape
+                if base is not None:
+                    base.data = torch.empty((1,), dtype=base.dtype, device=base.device)
+                t.data = torch.empty((1,), dtype=t.dtype, device=t.device)
+                self.stats["deallocated_outputs"] += 1
+            else:
+                held += t.untyped_storage().nbytes()
+        env["__held_bytes__"] = held
+        self.stats["held_output_bytes"] += held
+        self.stats["held_output_bytes_peak"] = max(self.stats["held_output_bytes_peak"],
+                                                   self.stats["held_output_bytes"])
+
+    def _release_outputs(self, env, s) -> None:
+        self.stats["held_output_bytes"] -= env.pop("__held_bytes__", 0)
 
     def _build_shared_groups(self):
         """One group per cross-stage shared parameter set, created collectively over every PP mesh
