@@ -29,6 +29,13 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# Micro-batch per TP degree: TP shrinks every per-rank GEMM and the attention head count, so the
+# TP=4/8 ranks process several sequences per micro-batch to keep MFMA tiles and the attention grid
+# full (global batch unchanged).  Per-GPU compute-only throughput at TP-8 shapes, mbs 1 / 2 / 4 / 8:
+# 367k / 391k / 415k / 414k tokens/s; TP-4 219k / 229k / 233k / 231k; TP-2 120k / 124k / 122k;
+# TP-1 63k / 63k (profiles/r2_mbs_sweep.jsonl, 8 layers).  TP-1 keeps 1: +1 % is not worth 10 GiB.
+MBS_BY_TP = {1: 1, 2: 2, 4: 4, 8: 4}
+
 BASELINE_TOKENS_PER_S = None  # the reference publishes no Llama-3-8B throughput
 
 
@@ -39,7 +46,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--seq", type=int, default=8192)
-    ap.add_argument("--mbs", type=int, default=1, help="micro-batch size (sequences)")
+    ap.add_argument("--mbs", type=int, default=None,
+                    help="micro-batch size (sequences); default per TP degree (MBS_BY_TP)")
     ap.add_argument("--gbs", type=int, default=8, help="global batch (sequences per optimizer step)")
     ap.add_argument("--parallelism", choices=["tp", "dp"], default="tp")
     ap.add_argument("--layers", type=int, default=None, help="override #layers (NOT the headline config)")
@@ -111,6 +119,9 @@ def main(a):
     if not use_cuda:
         torch.set_num_threads(max(1, (os.cpu_count() or 1) // world))
     backend = "nccl" if use_cuda else "gloo"
+    from neuronx_distributed_llama3_2_amd.parallel.rccl_env import apply_rccl_env
+
+    apply_rccl_env()
     dist.init_process_group(backend, rank=rank, world_size=world,
                             device_id=torch.device("cuda", local_rank) if use_cuda else None)
     dev = torch.device("cuda", local_rank) if use_cuda else torch.device("cpu")
@@ -142,6 +153,8 @@ def main(a):
     opt = FlatMixedPrecisionAdamW([{"params": decay, "weight_decay": 0.01}, {"params": no_decay, "weight_decay": 0.0}],
                                   lr=1e-5, betas=(0.9, 0.95), eps=1e-8, zero1=dp > 1, grad_clipping=True,
                                   max_grad_norm=1.0, shared_param_ids=find_shared_params(model))
+    if a.mbs is None:
+        a.mbs = max(1, min(MBS_BY_TP.get(tp, 1), a.gbs // dp))
     if a.gbs % (a.mbs * dp):
         raise SystemExit(f"bench: global batch {a.gbs} not divisible by micro-batch {a.mbs} x DP {dp}")
     accum = a.gbs // (a.mbs * dp)

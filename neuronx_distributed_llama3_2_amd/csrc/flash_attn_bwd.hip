@@ -611,7 +611,12 @@ int choose_chunk(int nkb, int Sq, int G, int causal, int off, int BH, int ncu) {
   int best = max_it;
   double best_t = 1e300;
   std::vector<double> fin;
-  for (int chunk = 8; chunk <= max_it; chunk = chunk < 64 ? chunk + 4 : chunk + chunk / 16) {
+  // measured (profiles/r2_fa_batch_chunks.jsonl): long items run far slower per iteration than
+  // this model says (32 q / 8 kv heads, B = 2: chunk 991 = 226 TF vs chunk 64 = 496 TF) -- their
+  // Q/dO streams lose the cross-item L2 reuse -- so the search is capped at kMaxChunk
+  constexpr int kMaxChunk = 160;
+  best = std::min(best, kMaxChunk);
+  for (int chunk = 8; chunk <= std::min(max_it, kMaxChunk); chunk = chunk < 64 ? chunk + 4 : chunk + chunk / 16) {
     const int64_t approx_items = (total + chunk - 1) / chunk;
     if (approx_items > 64 * (int64_t)ncu) continue;  // far too fine
     // min-heap of CU finish times
@@ -642,12 +647,30 @@ int choose_chunk(int nkb, int Sq, int G, int causal, int off, int BH, int ncu) {
   return best;
 }
 
+// tuning knobs, resolved once at load (NXD_FAB_ABLATE / NXD_FAB_CHUNK) and settable from Python
+// (flash_attn_set_knob) for in-process A/B — no per-launch getenv
+static int g_ablate = -1, g_chunk = -1;
 int ablate_flags() {
-  const char* e = getenv("NXD_FAB_ABLATE");  // re-read per launch (A/B in one process)
-  return e ? atoi(e) : 0;
+  if (g_ablate < 0) {
+    const char* e = getenv("NXD_FAB_ABLATE");
+    g_ablate = e ? atoi(e) : 0;
+  }
+  return g_ablate;
+}
+int chunk_override() {
+  if (g_chunk < 0) {
+    const char* e = getenv("NXD_FAB_CHUNK");
+    g_chunk = e ? atoi(e) : 0;
+  }
+  return g_chunk;
 }
 
 }  // namespace fab
+
+void flash_attn_bwd_set_knob(int which, int value) {
+  if (which == 0) fab::g_ablate = value;
+  if (which == 1) fab::g_chunk = value;
+}
 
 // fp32 workspace floats the backward needs: dq_acc + dk_acc + dv_acc + nlse + ndelta
 int64_t flash_attn_bwd_workspace(int B, int Sq, int Sk, int Hq, int Hkv, int D) {
@@ -699,7 +722,7 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   p.scale_log2 = softmax_scale * 1.4426950408889634f;
   p.causal = causal; p.causal_offset = causal_offset;
 
-  p.chunk = choose_chunk(nkb, Sq, G, causal, causal_offset, B * Hkv, num_cus());
+  p.chunk = chunk_override() > 0 ? chunk_override() : choose_chunk(nkb, Sq, G, causal, causal_offset, B * Hkv, num_cus());
   int64_t items = 0;
   for (int kb = 0; kb < nkb; ++kb) items += (kb_iters(kb, Sq, G, causal, causal_offset) + p.chunk - 1) / p.chunk;
   items *= (int64_t)B * Hkv;

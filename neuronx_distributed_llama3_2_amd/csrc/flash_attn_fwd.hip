@@ -410,6 +410,17 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
 
 }  // namespace fa
 
+// NXD_FA_FWD_VARIANT resolved once at load; flash_attn_set_knob(2, v) switches it for A/B runs
+static int g_fwd_variant = -1;
+static int fwd_variant() {
+  if (g_fwd_variant < 0) {
+    const char* e = getenv("NXD_FA_FWD_VARIANT");
+    g_fwd_variant = e ? atoi(e) : 13;
+  }
+  return g_fwd_variant;
+}
+void flash_attn_fwd_set_variant(int v) { g_fwd_variant = v; }
+
 int flash_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse,
                           const int64_t* qs, const int64_t* ks, const int64_t* vs, const int64_t* os,
                           int B, int Sq, int Sk, int Hq, int Hkv, int D, float softmax_scale,
@@ -438,8 +449,7 @@ int flash_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, 
   // priority for waves 4-7, 16 = 3-stage LDS ring, 32 = 128-key LDS tiles.  Measured at S=8192
   // D=128 causal, 32 / 4 heads (profiles/r1_fa_fwd_variants.jsonl): 0: 501 / 301 TF, 1: 531 / 298,
   // 5: 578 / 411, 13: 574-587 / 406-417; 2, 16, 32 measured neutral or slower (kept selectable).
-  const char* e = getenv("NXD_FA_FWD_VARIANT");
-  const int var = e ? atoi(e) : 13;
+  const int var = fwd_variant();
   const bool prio = var & 2;
   const bool pipe = var & 4;
   const bool ring3 = (var & 16) && pipe;

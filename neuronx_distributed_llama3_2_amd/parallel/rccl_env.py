@@ -1,0 +1,68 @@
+"""RCCL (torch.distributed "nccl" backend on ROCm) environment for a single MI355X node.
+
+Eight MI355X in a node are fully connected by xGMI: 7 point-to-point links per GPU, no switch.
+A ring collective therefore runs at the rate of ONE link per direction per channel, and the
+knob that matters is how many channels (= RCCL workgroups, i.e. CUs taken from compute) each
+collective uses.  The chunked SP overlap (parallel_layers/sp.py) wants collectives that leave
+most CUs to the concurrent GEMM; a pure comm benchmark wants many channels.  Both are settable:
+
+    NXD_RCCL_CHANNELS=<n>   -> NCCL_MIN_NCHANNELS = NCCL_MAX_NCHANNELS = n   (unset: RCCL picks)
+    NXD_COMM_HIGH_PRIORITY  -> TP / EP groups get high-priority RCCL streams (default 1;
+                               parallel_layers/parallel_state.py)
+
+`apply_rccl_env()` sets library defaults BEFORE `init_process_group` without overriding anything
+the user exported; `log_comm_config()` logs the effective RCCL-related environment once per
+process, so every run records the configuration its numbers were taken with.
+"""
+
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+from ..utils.logger import get_logger
+
+logger = get_logger()
+
+# defaults that are safe for any workload on one node
+RCCL_DEFAULTS: Dict[str, str] = {
+    # the dmabuf IPC path is the only one the ROCm driver on these nodes supports
+    "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+    # stash collective inputs in the work object instead of recordStream-ing them into the
+    # caching allocator (no cross-stream free-list fragmentation under async SP collectives)
+    "TORCH_NCCL_AVOID_RECORD_STREAMS": "1",
+}
+
+_PREFIXES = ("NCCL_", "RCCL_", "TORCH_NCCL_", "NXD_RCCL", "NXD_COMM", "NXD_SP_CHUNKS", "HSA_ENABLE_IPC")
+_logged = False
+
+
+def apply_rccl_env(extra: Optional[Dict[str, str]] = None) -> Dict[str, str]:
+    """Set the library's RCCL defaults (and `extra`) where the environment does not already
+    define them.  Returns what was set.  Call before `torch.distributed.init_process_group`."""
+    want = dict(RCCL_DEFAULTS)
+    ch = os.environ.get("NXD_RCCL_CHANNELS")
+    if ch:
+        want["NCCL_MIN_NCHANNELS"] = ch
+        want["NCCL_MAX_NCHANNELS"] = ch
+    if extra:
+        want.update(extra)
+    applied = {}
+    for k, v in want.items():
+        if k not in os.environ:
+            os.environ[k] = str(v)
+            applied[k] = str(v)
+    return applied
+
+
+def comm_config() -> Dict[str, str]:
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith(_PREFIXES)}
+
+
+def log_comm_config(force: bool = False) -> Dict[str, str]:
+    global _logged
+    cfg = comm_config()
+    if force or not _logged:
+        _logged = True
+        logger.info("> communication environment: %s", " ".join(f"{k}={v}" for k, v in cfg.items()) or "(defaults)")
+    return cfg

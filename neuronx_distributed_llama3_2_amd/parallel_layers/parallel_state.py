@@ -74,11 +74,26 @@ def _build_meshes(world_size: int, tp: int, pp: int, ep: int):
     return dp, edp, tp_mesh, dp_mesh, pp_mesh, ep_mesh, edp_mesh
 
 
-def _assign(mesh: List[List[int]], rank: int, backend=None):
+def _comm_options(high_priority: bool):
+    """RCCL group options: the groups whose collectives overlap GEMMs (TP/SP, EP all-to-all) get a
+    high-priority HIP stream, so the RCCL kernels are dispatched ahead of queued compute work
+    (NXD_COMM_HIGH_PRIORITY=0 turns it off)."""
+    if not high_priority or os.environ.get("NXD_COMM_HIGH_PRIORITY", "1") != "1":
+        return None
+    if dist.get_backend() != "nccl" or not hasattr(dist, "ProcessGroupNCCL"):
+        return None
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True
+    return opts
+
+
+def _assign(mesh: List[List[int]], rank: int, backend=None, high_priority: bool = False):
     """Create one group per mesh row (collectively on every rank) and return the one containing `rank`."""
     mine = None
+    opts = _comm_options(high_priority) if backend is None else None
     for ranks in mesh:
-        g = dist.new_group(ranks, backend=backend)
+        g = dist.new_group(ranks, backend=backend, pg_options=opts) if opts is not None else \
+            dist.new_group(ranks, backend=backend)
         if rank in ranks:
             mine = g
     return mine
@@ -100,10 +115,13 @@ def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_mode
     if ep > 1:
         logger.info("> initializing expert model parallel with size %d (expert data parallel %d)", ep, edp)
     _TP_MESH, _DP_MESH, _PP_MESH, _EP_MESH, _EDP_MESH = tp_mesh, dp_mesh, pp_mesh, ep_mesh, edp_mesh
-    _TP_GROUP = _assign(tp_mesh, rank)
+    from ..parallel.rccl_env import log_comm_config
+
+    log_comm_config()
+    _TP_GROUP = _assign(tp_mesh, rank, high_priority=True)
     _DP_GROUP = _assign(dp_mesh, rank)
     _PP_GROUP = _assign(pp_mesh, rank)
-    _EP_GROUP = _assign(ep_mesh, rank)
+    _EP_GROUP = _assign(ep_mesh, rank, high_priority=True)
     _EDP_GROUP = _assign(edp_mesh, rank)
     for ranks in pp_mesh:
         if rank in ranks:

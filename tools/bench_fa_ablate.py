@@ -36,7 +36,7 @@ def main():
         times = {n: [] for n in VARIANTS}
         for rep in range(5):
             for n, f in VARIANTS.items():
-                os.environ["NXD_FAB_ABLATE"] = str(f)
+                ext.flash_attn_set_knob(0, f)
                 run()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -46,7 +46,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 times[n].append(e0.elapsed_time(e1) / 5)
-        os.environ["NXD_FAB_ABLATE"] = "0"
+        ext.flash_attn_set_knob(0, 0)
         flops = 2.5 * 4 * B * Hq * S * S * D / 2
         for n, t in times.items():
             m = sorted(t)[len(t) // 2]

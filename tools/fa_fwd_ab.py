@@ -15,11 +15,11 @@ for (Hq, Hkv) in ((32, 8), (4, 1)):
     q = torch.randn(1, S, Hq, D, device="cuda", dtype=torch.bfloat16)
     k = torch.randn(1, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
     v = torch.randn(1, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
-    os.environ["NXD_FA_FWD_VARIANT"] = "0"
+    ops.ext().flash_attn_set_knob(2, 0)
     ref, _ = ops.flash_attn_fwd_lse(q, k, v, causal=True)
     fl = 4 * Hq * S * S * D / 2
     for var in sys.argv[1:] or ["0", "1", "2", "3"]:
-        os.environ["NXD_FA_FWD_VARIANT"] = var
+        ops.ext().flash_attn_set_knob(2, int(var))
         o, _ = ops.flash_attn_fwd_lse(q, k, v, causal=True)
         err = float((o.float() - ref.float()).abs().max())
         t = timeit(lambda: ops.flash_attn_fwd_lse(q, k, v, causal=True), iters=30)

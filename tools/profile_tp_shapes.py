@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--mbs", type=int, nargs="+", default=[1], help="micro-batch sizes (sequences) to time")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
@@ -38,21 +39,26 @@ def main():
                            num_hidden_layers=a.layers, max_position_embeddings=max(8192, a.seq))
         model = LlamaForCausalLM(cfg, dtype=torch.bfloat16, device=dev)
         model.train()
-        ids = torch.randint(0, cfg.vocab_size, (1, a.seq), device=dev)
+        for mbs in a.mbs:
+            ids = torch.randint(0, cfg.vocab_size, (mbs, a.seq), device=dev)
 
-        def mb():
-            out = model(ids, labels=ids)
-            out.loss.backward()
+            def mb():
+                out = model(ids, labels=ids)
+                out.loss.backward()
 
-        mb()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(a.iters):
             mb()
-        torch.cuda.synchronize()
-        ms = 1000 * (time.perf_counter() - t0) / a.iters
-        print(json.dumps({"tp_shapes": tp, "seq": a.seq, "layers": a.layers, "ms_per_microbatch_fwd_bwd": round(ms, 2),
-                          "tokens_per_s_per_gpu_compute_only": round(a.seq / ms * 1000 / 1, 1)}), flush=True)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.iters):
+                mb()
+            torch.cuda.synchronize()
+            ms = 1000 * (time.perf_counter() - t0) / a.iters
+            print(json.dumps({"tp_shapes": tp, "mbs": mbs, "seq": a.seq, "layers": a.layers,
+                              "ms_per_microbatch_fwd_bwd": round(ms, 2),
+                              "tokens_per_s_per_gpu_compute_only": round(mbs * a.seq / ms * 1000, 1),
+                              "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)}), flush=True)
+            del ids
+            torch.cuda.reset_peak_memory_stats(dev)
         del model
         torch.cuda.empty_cache()
     dist.destroy_process_group()

@@ -22,13 +22,13 @@ def cat(name: str) -> str:
     return "other:" + n[:60]
 
 
-def main(path):
+def main(path, split="adamw_kernel", by_kernel=False):
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    adam = [i for i, r in enumerate(rows) if "adamw_kernel" in r[2]]
+    adam = [i for i, r in enumerate(rows) if split in r[2]]
     # group adam launches into steps (consecutive launches within a short index distance)
     groups = []
     for i in adam:
@@ -36,14 +36,18 @@ def main(path):
             groups[-1].append(i)
         else:
             groups.append([i])
-    start = groups[-2][-1] + 1 if len(groups) >= 2 else 0
-    end = groups[-1][-1] + 1
+    if split == "adamw_kernel":
+        start = groups[-2][-1] + 1 if len(groups) >= 2 else 0
+        end = groups[-1][-1] + 1
+    else:   # e.g. "emb": from the last forward's first kernel group to the end of the trace
+        start, end = groups[-1][0], len(rows)
     sel = rows[start:end]
     tot = defaultdict(float)
     cnt = defaultdict(int)
     for s, e, n in sel:
-        tot[cat(n)] += (e - s) / 1e6
-        cnt[cat(n)] += 1
+        k = n[:110] if by_kernel else cat(n)
+        tot[k] += (e - s) / 1e6
+        cnt[k] += 1
     wall = (sel[-1][1] - sel[0][0]) / 1e6
     busy = sum(tot.values())
     print(f"last step: {len(sel)} kernels, wall {wall:.1f} ms, kernel-busy {busy:.1f} ms")
@@ -52,4 +56,12 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--split", default="adamw_kernel", help="kernel-name marker of a step boundary ('emb' for a"
+                    " forward+backward micro-batch trace without optimizer)")
+    ap.add_argument("--by-kernel", action="store_true")
+    a = ap.parse_args()
+    main(a.trace, a.split, a.by_kernel)
