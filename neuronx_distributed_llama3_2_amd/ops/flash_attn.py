@@ -122,6 +122,9 @@ class RopeAttentionFunc(torch.autograd.Function):
             rope_inplace_(flat, 0, nq + nkv, D, cos_t, sin_t,
                           (torch.arange(S * B, device=qkv.device) // B + position_offset))
         ctx.mark_dirty(qkv)
+        # the rotated qkv output is never differentiated through: do not let autograd zero-fill
+        # a [S, B, W] gradient for it every layer
+        ctx.set_materialize_grads(False)
         q, k, v = _views(qkv, nq, nkv, D)
         o = torch.empty((S, B, nq * D), dtype=qkv.dtype, device=qkv.device)
         o_v = o.view(S, B, nq, D).permute(1, 0, 2, 3)

@@ -39,12 +39,18 @@ def main():
                            num_hidden_layers=a.layers, max_position_embeddings=max(8192, a.seq))
         model = LlamaForCausalLM(cfg, dtype=torch.bfloat16, device=dev)
         model.train()
+        # the flat fp32 gradient buffers of the real training step (main_grad, hipBLASLt fp32
+        # in-place wgrad) -- never stepped, just zeroed between micro-batches
+        from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW
+
+        opt = FlatMixedPrecisionAdamW(model.parameters(), lr=0.0)
         for mbs in a.mbs:
             ids = torch.randint(0, cfg.vocab_size, (mbs, a.seq), device=dev)
 
             def mb():
                 out = model(ids, labels=ids)
                 out.loss.backward()
+                opt.zero_grad()
 
             mb()
             torch.cuda.synchronize()
@@ -59,7 +65,7 @@ def main():
                               "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)}), flush=True)
             del ids
             torch.cuda.reset_peak_memory_stats(dev)
-        del model
+        del model, opt
         torch.cuda.empty_cache()
     dist.destroy_process_group()
 
