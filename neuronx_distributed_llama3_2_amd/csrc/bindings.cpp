@@ -11,6 +11,7 @@ int flash_attn_fwd_launch(const void*, const void*, const void*, void*, float*, 
                           const int64_t*, const int64_t*, int, int, int, int, int, int, float, int, int, hipStream_t);
 int64_t flash_attn_bwd_workspace(int, int, int, int, int, int);
 void flash_attn_bwd_set_knob(int, int);
+int transpose_bf16_launch(const void*, void*, int64_t, int64_t, int64_t, int64_t, hipStream_t);
 void flash_attn_fwd_set_variant(int);
 int flash_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*, float*,
                           void*, void*, void*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
@@ -206,6 +207,20 @@ void rope_inplace(at::Tensor buf, int64_t T, int64_t W, int64_t col0, int64_t nh
   check_rc(nxd::rope_inplace_launch(buf.data_ptr(), T, W, (int)col0, (int)nheads, (int)D, cos_t.data_ptr<float>(),
                                     sin_t.data_ptr<float>(), pp, pos_div, pos_mod, (float)sign, cur_stream()),
            "rope");
+}
+
+// dst [C, R] = src [R, C]^T (bf16, unit inner strides, row strides multiples of 8 elements)
+void transpose_bf16(at::Tensor src, at::Tensor dst) {
+  check_bf16(src, "src");
+  check_bf16(dst, "dst");
+  TORCH_CHECK(src.dim() == 2 && dst.dim() == 2, "transpose_bf16: 2-D tensors");
+  TORCH_CHECK(src.stride(1) == 1 && dst.stride(1) == 1, "transpose_bf16: unit inner stride");
+  TORCH_CHECK(dst.size(0) == src.size(1) && dst.size(1) == src.size(0), "transpose_bf16: shape mismatch");
+  check_aligned16(src, "src");
+  check_aligned16(dst, "dst");
+  check_rc(nxd::transpose_bf16_launch(src.data_ptr(), dst.data_ptr(), src.size(0), src.size(1), src.stride(0),
+                                      dst.stride(0), cur_stream()),
+           "transpose_bf16");
 }
 
 void swiglu_fwd(at::Tensor gu, at::Tensor h) {
@@ -564,6 +579,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("rope_inplace", &rope_inplace);
   m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("transpose_bf16", &transpose_bf16);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("xent_stats", &xent_stats);
   m.def("xent_bwd", &xent_bwd);

@@ -116,7 +116,7 @@ class GQAQKVLinearWithAsyncCommunication(torch.autograd.Function):
             # dgrad GEMM chunks with their reduce-scatters in flight behind them
             grad_input, handles = sp.matmul_reduce_scatter_start(grad_output, weight, group)
         else:
-            grad_input = _gemm.matmul(grad_output, weight)
+            grad_input = _gemm.dgrad(grad_output, weight)
             if ctx.async_grad_allreduce and ws > 1:
                 handles = [dist.all_reduce(grad_input, group=group, async_op=True)]
         go2 = grad_output.reshape(-1, grad_output.shape[-1])

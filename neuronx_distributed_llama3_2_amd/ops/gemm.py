@@ -54,8 +54,23 @@ _WGRAD_BF16 = os.environ.get("NXD_WGRAD_BF16", "0") == "1"
 _scratch = {}
 
 
-def _wgrad_scratch(n: int, dtype, device) -> torch.Tensor:
-    key = (dtype, str(device))
+# wgrad through transposed operands pays when the GEMM time saved, ~0.39e-15 * T*N*K s, beats the
+# two transposes, ~0.8e-12 * T*(N+K) s: N*K/(N+K) above ~2200 (Llama-3-8B: gate_up, down, qkv and
+# lm_head at TP=1; none of the TP=8 shards).  NXD_WGRAD_T=0 disables, =2 forces.
+_WGRAD_T = os.environ.get("NXD_WGRAD_T", "1")
+
+
+def _use_wgrad_t(go2: torch.Tensor, x2: torch.Tensor) -> bool:
+    if _WGRAD_T == "0" or _WGRAD_BF16:
+        return False
+    T, N, K = go2.shape[0], go2.shape[1], x2.shape[1]
+    if T % 8 or N % 8 or K % 8 or go2.stride(-1) != 1 or x2.stride(-1) != 1 or go2.stride(0) % 8 or x2.stride(0) % 8:
+        return False
+    return _WGRAD_T == "2" or N * K / (N + K) > 2200
+
+
+def _wgrad_scratch(n: int, dtype, device, tag: str = "") -> torch.Tensor:
+    key = (dtype, str(device), tag)
     t = _scratch.get(key)
     if t is None or t.numel() < n:
         t = _scratch[key] = torch.empty(n, dtype=dtype, device=device)
@@ -70,6 +85,14 @@ def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor) -> 
     bf16 before the fp32 accumulation — the precision of the reference's XLA matmul + fp32
     grad accumulation; hipBLASLt's bf16-output solutions run faster than its fp32-output ones)."""
     if _native(go2, x2) and mg.is_contiguous():
+        if _use_wgrad_t(go2, x2):
+            # T-contiguous operands: both transposed by the HIP kernel (~5 TB/s) into scratch, then
+            # the TN GEMM (1.30-1.44 vs 1.06-1.16 PF/s on the NT layout, profiles/r2_gemm_layouts)
+            T, N, K = go2.shape[0], go2.shape[1], x2.shape[1]
+            gt = transpose(go2, out=_wgrad_scratch(N * T, go2.dtype, go2.device, "gt").view(N, T))
+            xt = transpose(x2, out=_wgrad_scratch(K * T, x2.dtype, x2.device, "xt").view(K, T))
+            ext().gemm(gt, xt.t(), mg, None, 1.0, 1.0)
+            return
         if _WGRAD_BF16:
             tmp = _wgrad_scratch(mg.numel(), go2.dtype, go2.device).view(mg.shape)
             ext().gemm(go2.t(), x2, tmp, None, 1.0, 0.0)
@@ -81,3 +104,53 @@ def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor) -> 
         torch.addmm(mg, go2.t(), x2, out_dtype=torch.float32, out=mg)
     else:
         mg.add_(go2.t().float().matmul(x2.float()))
+
+
+# ----------------------------------------------------------------------------- dgrad layout
+# hipBLASLt runs dX = dY W (W [N, K] row-major: the contraction dim is W's row dim) at 1.31-1.44
+# PF/s on the Llama-3-8B shapes but at 1.56-1.69 PF/s when W is stored K-major (W^T [K, N]
+# contiguous; profiles/r2_gemm_layouts.jsonl).  Training therefore keeps a K-major copy of every
+# weight it back-propagates through, refreshed lazily by the first backward after the weights
+# changed (one transpose per weight per optimizer step, HBM-bound, vs a faster dgrad in every
+# micro-batch).  Staleness is detected by the optimizer's weight epoch (bumped by every optimizer
+# step and checkpoint load that writes the weights outside autograd) plus the tensor's own
+# version counter and storage pointer (any in-place torch write).  NXD_DGRAD_WT=0 disables it.
+_DGRAD_WT = os.environ.get("NXD_DGRAD_WT", "1") == "1"
+_weight_epoch = [0]
+
+
+def weights_updated() -> None:
+    """Tell the GEMM layer that weights were rewritten behind autograd's back (optimizer step)."""
+    _weight_epoch[0] += 1
+
+
+def transpose(src: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """[R, C] -> contiguous [C, R] (HIP tiled transpose for bf16; torch elsewhere)."""
+    dst = out if out is not None else torch.empty((src.shape[1], src.shape[0]), dtype=src.dtype, device=src.device)
+    if use_native(src) and src.dtype == torch.bfloat16 and src.stride(-1) == 1 and src.shape[0] % 8 == 0 \
+            and src.shape[1] % 8 == 0 and src.stride(0) % 8 == 0:
+        ext().transpose_bf16(src, dst)
+    else:
+        dst.copy_(src.t())
+    return dst
+
+
+def _kmajor(weight: torch.Tensor) -> torch.Tensor:
+    key = (_weight_epoch[0], weight._version, weight.data_ptr())
+    wt = getattr(weight, "_nxd_wt", None)
+    if wt is None or getattr(weight, "_nxd_wt_key", None) != key:
+        if wt is None or wt.shape != (weight.shape[1], weight.shape[0]):
+            wt = torch.empty((weight.shape[1], weight.shape[0]), dtype=weight.dtype, device=weight.device)
+        transpose(weight.detach(), out=wt)
+        weight._nxd_wt = wt
+        weight._nxd_wt_key = key
+    return wt
+
+
+def dgrad(go: torch.Tensor, weight: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """dX = go [..., N] @ weight [N, K] -> [..., K] (the input gradient of y = x W^T)."""
+    if _DGRAD_WT and _native(go, weight) and go.stride(-1) == 1 and weight.dim() == 2 and weight.shape[0] % 8 == 0 \
+            and weight.shape[1] % 8 == 0 and weight.is_contiguous():
+        wt = _kmajor(weight)
+        return matmul(go, wt.t(), out=out)
+    return matmul(go, weight, out=out)

@@ -68,6 +68,9 @@ def adamw_flat_(p32: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, ex
                 step: int, grad_scale: Optional[torch.Tensor] = None, grad_scale_host: float = 1.0,
                 bias_correction: bool = True) -> None:
     """In-place AdamW (decoupled weight decay) over flat fp32 buffers; writes bf16 params to p16."""
+    from .gemm import weights_updated
+
+    weights_updated()   # the kernel writes weights behind autograd: K-major dgrad copies go stale
     bc1 = 1.0 - beta1 ** step if bias_correction else 1.0
     bc2 = 1.0 - beta2 ** step if bias_correction else 1.0
     if use_native(p32, grad):

@@ -199,6 +199,9 @@ class FlatBuffer:
         """ZeRO-1: all-gather every bucket's updated bf16 slices (in place)."""
         if not self.zero1:
             return
+        from ..ops.gemm import weights_updated
+
+        weights_updated()
         handles = []
         for b in self.buckets:
             n = (b.end - b.start) // self.dp

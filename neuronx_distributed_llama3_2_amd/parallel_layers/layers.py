@@ -147,7 +147,7 @@ class LinearWithAsyncCommunication(torch.autograd.Function):
         if ctx.sequence_parallel_enabled and dist.get_world_size(group=group) > 1:
             grad_input, handles = sp.matmul_reduce_scatter_start(grad_output, weight, group)
         else:
-            grad_input = _gemm.matmul(grad_output, weight)
+            grad_input = _gemm.dgrad(grad_output, weight)
             if not ctx.sequence_parallel_enabled and ctx.async_grad_allreduce and dist.get_world_size(group=group) > 1:
                 handles = [dist.all_reduce(grad_input, group=group, async_op=True)]
         go2 = grad_output.reshape(-1, grad_output.shape[-1])

@@ -145,14 +145,14 @@ def gather_matmul(g_local: torch.Tensor, weight: torch.Tensor, group=None) -> Tu
     """Row-parallel SP backward: (all-gather(g_local) @ weight, gathered g), chunk-pipelined."""
     group = group if group is not None else get_tensor_model_parallel_group()
     if _ws(group) == 1:
-        return _gemm.matmul(g_local, weight), g_local
+        return _gemm.dgrad(g_local, weight), g_local
     full, hs, c = gather_start(g_local, group)
     out = torch.empty(tuple(full.shape[:-1]) + (weight.shape[1],), dtype=full.dtype, device=full.device)
     fv = full.view((c, full.shape[0] // c) + tuple(full.shape[1:]))
     ov = out.view((c, out.shape[0] // c) + tuple(out.shape[1:]))
     for j in range(c):
         hs[j].wait()
-        _gemm.matmul(fv[j], weight, out=ov[j])
+        _gemm.dgrad(fv[j], weight, out=ov[j])
     return out, full
 
 
@@ -185,4 +185,4 @@ def matmul_reduce_scatter_start(g_full: torch.Tensor, weight: torch.Tensor, grou
     """Column-parallel SP backward: reduce_scatter(g_full @ weight), chunk-pipelined."""
     group = group if group is not None else get_tensor_model_parallel_group()
     g_full = g_full.contiguous()
-    return _gemm_reduce_scatter(lambda a, o: _gemm.matmul(a, weight, out=o), g_full, weight.shape[1], group)
+    return _gemm_reduce_scatter(lambda a, o: _gemm.dgrad(a, weight, out=o), g_full, weight.shape[1], group)

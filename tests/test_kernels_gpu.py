@@ -340,3 +340,52 @@ def test_argmax_large_vocab():
     x[2, 5] = x[2, 128255] = 60.0  # tie -> smallest index
     a = ops.argmax_rows(x)
     assert a.tolist() == [int(x[0].float().argmax()), 77777, 5]
+
+
+@pytest.mark.parametrize("R,C", [(64, 64), (8192, 4096), (1000, 72), (4096, 14336)])
+def test_transpose_bf16(R, C):
+    from neuronx_distributed_llama3_2_amd.ops import gemm
+
+    x = torch.randn(R + 8, C, device=DEV, dtype=torch.bfloat16)[:R]   # padded row stride too
+    y = gemm.transpose(x)
+    assert torch.equal(y, x.t().contiguous())
+
+
+def test_dgrad_kmajor_weight_refreshes():
+    """dX = dY W through the cached K-major weight copy; stale copies are refreshed after an
+    optimizer-kernel update (epoch), an in-place torch write (version) and a .data swap."""
+    from neuronx_distributed_llama3_2_amd.ops import gemm
+
+    w = torch.nn.Parameter(torch.randn(768, 512, device=DEV, dtype=torch.bfloat16))
+    g = torch.randn(256, 768, device=DEV, dtype=torch.bfloat16)
+    ref = lambda: (g.float() @ w.detach().float())
+    assert _rel(gemm.dgrad(g, w), ref()) < 1e-2
+    # optimizer kernel writes the bf16 weights behind autograd
+    p32 = w.detach().float().reshape(-1).clone()
+    grad = torch.randn_like(p32)
+    ops.adamw_flat_(p32, grad, torch.zeros_like(p32), torch.zeros_like(p32), w.data.view(-1), 1e-1, 0.9, 0.95, 1e-8,
+                    0.0, 1)
+    assert _rel(gemm.dgrad(g, w), ref()) < 1e-2
+    with torch.no_grad():
+        w.mul_(-1.0)   # in-place torch write: version counter
+    assert _rel(gemm.dgrad(g, w), ref()) < 1e-2
+    w.data = torch.randn_like(w.data)   # new storage
+    assert _rel(gemm.dgrad(g, w), ref()) < 1e-2
+
+
+@pytest.mark.parametrize("mode", ["0", "2"])
+def test_wgrad_accumulate_layouts(mode, monkeypatch):
+    """fp32 main_grad += dY^T X through the NT GEMM (mode 0) and the transposed-operand TN GEMM
+    (mode 2) against an fp32 reference, accumulating over two micro-batches."""
+    from neuronx_distributed_llama3_2_amd.ops import gemm
+
+    monkeypatch.setattr(gemm, "_WGRAD_T", mode)
+    T, N, K = 512, 768, 256
+    mg = torch.zeros(N, K, device=DEV, dtype=torch.float32)
+    ref = torch.zeros(N, K, device=DEV, dtype=torch.float32)
+    for _ in range(2):
+        go = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
+        x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
+        gemm.wgrad_accumulate_(mg, go, x)
+        ref += go.float().t() @ x.float()
+    assert _rel(mg, ref) < 1e-3

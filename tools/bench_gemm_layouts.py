@@ -52,8 +52,10 @@ for name, (N, K) in shapes.items():
     r["wgradT_tf"] = fl / t(lambda: E.gemm(gt, xt.t(), mg, None, 1.0, 1.0)) / 1e9
     r["wgrad_ms"] = fl / r["wgrad_tf"] / 1e9
     r["wgradT_ms"] = fl / r["wgradT_tf"] / 1e9
-    r["transpose_g_ms"] = t(lambda: gt.copy_(g.t()))
-    r["transpose_x_ms"] = t(lambda: xt.copy_(x.t()))
+    r["transpose_g_ms_torch"] = t(lambda: gt.copy_(g.t()))
+    r["transpose_g_ms"] = t(lambda: E.transpose_bf16(g, gt))
+    r["transpose_x_ms"] = t(lambda: E.transpose_bf16(x, xt))
+    r["transpose_g_tbs"] = 2 * g.numel() * 2 / r["transpose_g_ms"] / 1e9
     print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}), flush=True)
     del x, w, g, mg, y, dx, wt, gt, xt
     torch.cuda.empty_cache()
