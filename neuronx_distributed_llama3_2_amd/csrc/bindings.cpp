@@ -47,6 +47,7 @@ int gemv_launch(const void*, int64_t, const void*, int64_t, int, const float*, f
 int dequant_int8_launch(const void*, int64_t, const float*, float, void*, int, int, hipStream_t);
 int expert_gemv_launch(const void*, int64_t, const void*, int64_t, int64_t, const int32_t*, int, int, void*, int64_t, int,
                        int, int, hipStream_t);
+int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, int, hipStream_t);
 }  // namespace nxd
 
 namespace {
@@ -556,6 +557,49 @@ void dequant_int8(at::Tensor w, c10::optional<at::Tensor> scale, double tscale, 
            "dequant_int8");
 }
 
+// MoE grouped GEMMs over expert-sorted rows (csrc/grouped_gemm.hip); offs int32 [E + 1] on device.
+//   mode 0: a = x [M, K], b = W [E, K, N], c = y [M, N] bf16
+//   mode 1: a = dy [M, N], b = W [E, K, N], c = dx [M, K] bf16
+//   mode 2: a = x [M, K], b = dy [M, N], c = dW [E, K, N] fp32 (accumulate: +=)
+void grouped_gemm(int64_t mode, at::Tensor a, at::Tensor b, at::Tensor offs, at::Tensor c, bool accumulate) {
+  check_bf16(a, "a");
+  check_bf16(b, "b");
+  check_cuda(c, "c");
+  check_cuda(offs, "offs");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && c.is_contiguous(), "grouped_gemm: contiguous operands");
+  TORCH_CHECK(offs.scalar_type() == at::kInt && offs.dim() == 1 && offs.is_contiguous(), "grouped_gemm: offs int32 [E+1]");
+  check_aligned16(a, "a");
+  check_aligned16(b, "b");
+  check_aligned16(c, "c");
+  TORCH_CHECK(a.dim() == 2, "grouped_gemm: a must be 2-D");
+  const int64_t M = a.size(0);
+  int64_t E, K, N;
+  if (mode == 0 || mode == 1) {
+    TORCH_CHECK(b.dim() == 3, "grouped_gemm: W must be [E, K, N]");
+    E = b.size(0); K = b.size(1); N = b.size(2);
+    check_bf16(c, "c");
+    TORCH_CHECK(c.dim() == 2 && c.size(0) == M, "grouped_gemm: output rows");
+    if (mode == 0) {
+      TORCH_CHECK(a.size(1) == K && c.size(1) == N, "grouped_gemm fwd: x [M, K], y [M, N]");
+    } else {
+      TORCH_CHECK(a.size(1) == N && c.size(1) == K, "grouped_gemm dgrad: dy [M, N], dx [M, K]");
+    }
+  } else if (mode == 2) {
+    TORCH_CHECK(b.dim() == 2 && b.size(0) == M, "grouped_gemm wgrad: dy [M, N]");
+    TORCH_CHECK(c.scalar_type() == at::kFloat && c.dim() == 3, "grouped_gemm wgrad: dW fp32 [E, K, N]");
+    E = c.size(0); K = a.size(1); N = b.size(1);
+    TORCH_CHECK(c.size(1) == K && c.size(2) == N, "grouped_gemm wgrad: dW shape");
+  } else {
+    TORCH_CHECK(false, "grouped_gemm: mode must be 0, 1 or 2");
+  }
+  TORCH_CHECK(offs.size(0) == E + 1, "grouped_gemm: offs must have E + 1 entries");
+  TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "grouped_gemm: K and N must be multiples of 8");
+  TORCH_CHECK(M < (1LL << 31) && K < (1LL << 31) && N < (1LL << 31) && E < 65536, "grouped_gemm: sizes too large");
+  check_rc(nxd::grouped_gemm_launch((int)mode, a.data_ptr(), b.data_ptr(), c.data_ptr(), offs.data_ptr<int32_t>(), (int)E,
+                                    (int)M, (int)K, (int)N, accumulate ? 1 : 0, cur_stream()),
+           "grouped_gemm");
+}
+
 }  // namespace
 
 void register_gemm(pybind11::module& m);  // gemm.cpp
@@ -567,6 +611,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemv", &gemv);
   m.def("dequant_int8", &dequant_int8);
   m.def("expert_gemv", &expert_gemv);
+  m.def("grouped_gemm", &grouped_gemm);
   m.doc() = "CDNA4 (gfx950) kernels of neuronx_distributed_llama3_2_amd";
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);

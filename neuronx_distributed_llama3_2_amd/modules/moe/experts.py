@@ -133,27 +133,17 @@ class ExpertMLPs(nn.Module):
         if ps.get_tensor_model_parallel_size() > 1 and not self.input_grad_reduced_by_caller:
             # experts are TP-sharded on I: input grads are partial sums over TP
             hidden_states = copy_to_tensor_model_parallel_region(hidden_states)
-        flat_e = expert_index.reshape(-1)                      # [T*k]
-        order = torch.argsort(flat_e, stable=True)
-        tok = order // k                                       # source token of each sorted slot
-        counts = torch.bincount(flat_e, minlength=self.num_experts).tolist()
-        x_sorted = hidden_states.index_select(0, tok)
+        # device-side permutation: stable sort of the T*k slots by expert, group offsets by a
+        # cumsum of the per-expert counts -- no group size ever reaches the host
+        order, inverse, offs = ops.moe_permutation(expert_index, self.num_experts)
+        x_sorted = hidden_states.index_select(0, order // k)
         w_gu, w_d = self.mlp_op.gate_up_proj.weight, self.mlp_op.down_proj.weight
-        outs = []
-        start = 0
-        for e, n in enumerate(counts):
-            if n == 0:
-                continue
-            xe = x_sorted[start:start + n]
-            he = self.mlp_op._activation(xe @ w_gu[e])
-            outs.append(he @ w_d[e])
-            start += n
-        y_sorted = torch.cat(outs, 0) if outs else hidden_states.new_zeros(0, H)
-        aff = self._chosen_affinities(expert_affinities, expert_index).reshape(-1)[order]
-        y_sorted = y_sorted * aff.unsqueeze(1).to(y_sorted.dtype)
-        out = torch.zeros(T, H, dtype=y_sorted.dtype, device=hidden_states.device)
-        out.index_add_(0, tok, y_sorted)
-        return out
+        h = self.mlp_op._activation(ops.grouped_linear(x_sorted, w_gu, offs))
+        y_sorted = ops.grouped_linear(h, w_d, offs)            # [T*k, H] TP-partial
+        # un-permute by gathering each (token, choice) slot, then the affinity-weighted sum over k
+        y = y_sorted.index_select(0, inverse).view(T, k, H)
+        aff = self._chosen_affinities(expert_affinities, expert_index).to(y.dtype)
+        return torch.einsum("tkh,tk->th", y, aff)
 
     def forward_all_experts(self, hidden_states, expert_affinities, expert_index):
         """Every token through every expert (reference semantics; used for tiny batches)."""
