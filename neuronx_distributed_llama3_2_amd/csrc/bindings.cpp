@@ -47,6 +47,11 @@ int gemv_launch(const void*, int64_t, const void*, int64_t, int, const float*, f
 int dequant_int8_launch(const void*, int64_t, const float*, float, void*, int, int, hipStream_t);
 int expert_gemv_launch(const void*, int64_t, const void*, int64_t, int64_t, const int32_t*, int, int, void*, int64_t, int,
                        int, int, hipStream_t);
+void dgemv_set_knob(int, int);
+void decode_attn_set_v2(int);
+int dgemv_launch(int, const void*, int64_t, const void*, float, const void*, int64_t, void*, int64_t, int, int, int, int,
+                 int, int, const float*, const float*, const int64_t*, int, void*, void*, int64_t, int64_t, int64_t,
+                 const int*, int, int, hipStream_t);
 int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, int, hipStream_t);
 }  // namespace nxd
 
@@ -600,6 +605,78 @@ void grouped_gemm(int64_t mode, at::Tensor a, at::Tensor b, at::Tensor offs, at:
            "grouped_gemm");
 }
 
+// Fused decode GEMV (csrc/decode_fused.hip).  epi: 0 plain, 1 residual add into y (in place),
+// 2 SwiGLU on a fused [2N, K] gate/up weight, 3 QKV with RoPE + KV-cache write.  norm_w: RMSNorm
+// of x fused as a prologue.  x [M, K], w [Nw, K], y [M, N] bf16, M <= 8.
+void dgemv(int64_t epi, at::Tensor x, c10::optional<at::Tensor> norm_w, double eps, at::Tensor w, at::Tensor y,
+           int64_t nq, int64_t nkv, int64_t D, c10::optional<at::Tensor> cos_t, c10::optional<at::Tensor> sin_t,
+           c10::optional<at::Tensor> pos, int64_t T, c10::optional<at::Tensor> kc, c10::optional<at::Tensor> vc,
+           c10::optional<at::Tensor> cache_idx) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "dgemv: x [M, K], w [Nw, K], y [M, N]");
+  TORCH_CHECK(x.stride(1) == 1 && w.stride(1) == 1 && y.stride(1) == 1, "dgemv: unit inner strides");
+  const int64_t M = x.size(0), K = x.size(1), N = y.size(1);
+  TORCH_CHECK(M >= 1 && M <= 8 && y.size(0) == M, "dgemv: 1..8 rows");
+  TORCH_CHECK(K % 8 == 0 && x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && w.size(1) == K, "dgemv: K / strides");
+  check_aligned16(x, "x");
+  check_aligned16(w, "w");
+  TORCH_CHECK(w.size(0) == (epi == 2 ? 2 * N : N), "dgemv: weight rows vs output columns");
+  const void* nw = nullptr;
+  if (norm_w.has_value()) {
+    check_bf16(*norm_w, "norm_w");
+    TORCH_CHECK(norm_w->is_contiguous() && norm_w->numel() == K, "dgemv: norm weight [K]");
+    check_aligned16(*norm_w, "norm_w");
+    TORCH_CHECK(M * K * 2 <= 65536, "dgemv: fused norm needs M * K <= 32768");
+    nw = norm_w->data_ptr();
+  }
+  const float *cp = nullptr, *sp = nullptr;
+  const int64_t* pp = nullptr;
+  void *kp = nullptr, *vp = nullptr;
+  const int* ci = nullptr;
+  int64_t c_sb = 0, c_sh = 0, c_sl = 0;
+  int Lmax = 0, max_pos = 0;
+  if (epi == 3) {
+    TORCH_CHECK(cos_t.has_value() && sin_t.has_value() && pos.has_value() && kc.has_value() && vc.has_value(),
+                "dgemv rope_kv: cos, sin, pos, k/v cache required");
+    TORCH_CHECK(D % 2 == 0 && D >= 2 && nq >= 1 && nkv >= 1 && N == (nq + 2 * nkv) * D, "dgemv rope_kv: head layout");
+    TORCH_CHECK(cos_t->scalar_type() == at::kFloat && sin_t->scalar_type() == at::kFloat && cos_t->is_contiguous() &&
+                    sin_t->is_contiguous() && cos_t->dim() == 2 && cos_t->size(1) == D / 2 && sin_t->sizes() == cos_t->sizes(),
+                "dgemv rope_kv: fp32 cos/sin tables [P, D/2]");
+    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->is_contiguous() && pos->numel() == M, "dgemv rope_kv: int64 pos [M]");
+    check_bf16(*kc, "k_cache");
+    check_bf16(*vc, "v_cache");
+    TORCH_CHECK(kc->dim() == 4 && kc->sizes() == vc->sizes() && kc->strides() == vc->strides() && kc->stride(3) == 1 &&
+                    kc->size(1) == nkv && kc->size(3) == D,
+                "dgemv rope_kv: caches [B, Hkv, Lmax, D]");
+    TORCH_CHECK(T >= 1 && M % T == 0, "dgemv rope_kv: rows must be whole sequences of T tokens");
+    if (cache_idx.has_value()) {
+      TORCH_CHECK(cache_idx->scalar_type() == at::kInt && cache_idx->is_contiguous() && cache_idx->numel() == M / T,
+                  "dgemv rope_kv: int32 cache_idx [B]");
+      ci = cache_idx->data_ptr<int>();
+    } else {
+      TORCH_CHECK(kc->size(0) >= M / T, "dgemv rope_kv: cache batch");
+    }
+    cp = cos_t->data_ptr<float>();
+    sp = sin_t->data_ptr<float>();
+    pp = pos->data_ptr<int64_t>();
+    kp = kc->data_ptr();
+    vp = vc->data_ptr();
+    c_sb = kc->stride(0);
+    c_sh = kc->stride(1);
+    c_sl = kc->stride(2);
+    Lmax = kc->size(2);
+    max_pos = cos_t->size(0);
+  } else {
+    TORCH_CHECK(epi >= 0 && epi <= 2, "dgemv: epi must be 0..3");
+  }
+  check_rc(nxd::dgemv_launch((int)epi, x.data_ptr(), x.stride(0), nw, (float)eps, w.data_ptr(), w.stride(0), y.data_ptr(),
+                             y.stride(0), (int)M, (int)N, (int)K, (int)nq, (int)nkv, (int)D, cp, sp, pp, (int)T, kp, vp,
+                             c_sb, c_sh, c_sl, ci, Lmax, max_pos, cur_stream()),
+           "dgemv");
+}
+
 }  // namespace
 
 void register_gemm(pybind11::module& m);  // gemm.cpp
@@ -612,6 +689,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("dequant_int8", &dequant_int8);
   m.def("expert_gemv", &expert_gemv);
   m.def("grouped_gemm", &grouped_gemm);
+  m.def("dgemv", &dgemv);
+  // decode A/B knobs: 0 = GLU row pairs per wave, 1 = GEMV k-slices (0 auto), 2 = MFMA decode attention on/off
+  m.def("decode_set_knob", [](int which, int value) {
+    if (which == 2) nxd::decode_attn_set_v2(value);
+    else nxd::dgemv_set_knob(which, value);
+  });
   m.doc() = "CDNA4 (gfx950) kernels of neuronx_distributed_llama3_2_amd";
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);

@@ -1,0 +1,263 @@
+// Decode attention on MFMA for small query groups (M = (Hq/Hkv) * T <= 16 rows per kv head):
+// one workgroup of 4 waves owns a (batch, kv head, key split of 1024 keys); every wave runs an
+// online-softmax flash-decoding loop over 64-key chunks entirely in registers:
+//
+//   S^T[key][m] = K.Q^T   v_mfma_f32_16x16x32_bf16, K rows straight from the cache (16-B loads),
+//                         Q^T fragments held for the whole loop (rows >= M are zero);
+//   softmax             16 scores per lane (4 key tiles x 4), row max / sum over the 4 lanes of a
+//                         query row with two xor-shuffles, exp2 with the scale folded in;
+//   O[m][d] += P.V      P re-packed into the A operand with 16 lane shuffles per chunk, V staged
+//                         through a per-wave LDS tile and read transposed (ds_read_b64_tr_b16);
+//
+// then the 4 waves merge their (max, sum, O) through LDS once.  With one split (cache <= 1024
+// keys) the workgroup writes the final bf16 output; otherwise it writes the (m, l, o) partials that
+// inference.hip's merge kernel combines.  Compared with the 128-key-chunk kernel there (four
+// workgroup barriers per chunk and a merge launch at every length) this is one barrier per call.
+#include "common.h"
+
+namespace nxd {
+namespace dattn {
+
+constexpr int KB = 64;            // keys per chunk (one wave)
+constexpr int KPS = 1024;         // keys per workgroup split
+
+struct Params {
+  const uint16_t* q;
+  int64_t q_sb, q_st, q_sh;
+  const uint16_t* kc;
+  const uint16_t* vc;
+  int64_t c_sb, c_sh, c_sl;
+  const int* cache_idx;
+  const int* seq_len;
+  uint16_t* out;
+  int64_t o_sb, o_st, o_sh;
+  float* po;   // [B*Hkv, nsplit, M, D] partials (nsplit > 1)
+  float* pm;   // natural-log row max
+  float* pl;
+  int B, T, Hq, Hkv, nsplit;
+  float scale_log2;   // softmax scale * log2(e)
+};
+
+typedef __attribute__((address_space(3))) short4_t lds_s4_t;
+typedef short short8_t __attribute__((ext_vector_type(8)));
+
+template <int D, int NWV>
+__global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
+  constexpr int NS = D / 32;      // k-steps of the score MFMA
+  constexpr int NDT = D / 16;     // 16-wide d tiles of the output
+  constexpr int VL = D / 8;       // 16-B V loads per lane for 64 keys x D
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int mi = lane & 15, g = lane >> 4;
+  uint16_t* vt = reinterpret_cast<uint16_t*>(smem) + wid * KB * D;              // this wave's V tile [64][D]
+  float* red_o = reinterpret_cast<float*>(smem + NWV * KB * D * 2);             // [NWV][16][D]
+  float* red_m = red_o + NWV * 16 * D;                                          // [NWV][16]
+  float* red_l = red_m + NWV * 16;
+
+  const int split = blockIdx.x % p.nsplit;
+  const int bh = blockIdx.x / p.nsplit;
+  const int b = bh / p.Hkv, hkv = bh % p.Hkv;
+  const int G = p.Hq / p.Hkv, M = G * p.T;
+  const int cb = p.cache_idx ? p.cache_idx[b] : b;
+  const int slen = p.seq_len[b];
+  const uint16_t* kbase = p.kc + (int64_t)cb * p.c_sb + (int64_t)hkv * p.c_sh;
+  const uint16_t* vbase = p.vc + (int64_t)cb * p.c_sb + (int64_t)hkv * p.c_sh;
+
+  // Q^T fragments: lane (mi, g) holds Q[mi][32 s + 8 g .. +7]
+  bf16x8_t qf[NS];
+  const int tt_q = mi / G, gg_q = mi % G;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    u32x4_t v = {0, 0, 0, 0};
+    if (mi < M)
+      v = *reinterpret_cast<const u32x4_t*>(p.q + (int64_t)b * p.q_sb + (int64_t)tt_q * p.q_st +
+                                             (int64_t)(hkv * G + gg_q) * p.q_sh + 32 * s + 8 * g);
+    qf[s] = __builtin_bit_cast(bf16x8_t, v);
+  }
+  const int lim = slen - (p.T - 1 - tt_q);        // keys visible to query row mi (causal over new tokens)
+
+  float run_m = -INFINITY, run_l = 0.f;           // stats of query row mi (log2 domain)
+  f32x4_t o[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) o[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int kend = min(slen, (split + 1) * KPS);
+  // K fragments and the V chunk of the NEXT chunk are loaded while this one runs its softmax and P.V
+  u32x4_t kf[4][NS], vv[VL];
+  auto load_chunk = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < VL; ++i) {
+      const int idx = lane + 64 * i, key = idx / (D / 8), c = idx % (D / 8);
+      vv[i] = *reinterpret_cast<const u32x4_t*>(vbase + (int64_t)min(k0 + key, slen - 1) * p.c_sl + 8 * c);
+    }
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const uint16_t* kr = kbase + (int64_t)min(k0 + kt * 16 + mi, slen - 1) * p.c_sl + 8 * g;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) kf[kt][s] = *reinterpret_cast<const u32x4_t*>(kr + 32 * s);
+    }
+  };
+  int k0 = split * KPS + wid * KB;
+  if (k0 < kend) load_chunk(k0);
+  for (; k0 < kend; k0 += NWV * KB) {
+    // ---- scores S^T[key][m] for 4 key tiles of 16
+    f32x4_t sc[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      sc[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        sc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kf[kt][s]), qf[s], sc[kt], 0, 0, 0);
+    }
+    // V tile -> LDS (row-major [key][D]) once the wave's previous transposed reads have retired
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < VL; ++i) {
+      const int idx = lane + 64 * i, key = idx / (D / 8), c = idx % (D / 8);
+      *reinterpret_cast<u32x4_t*>(vt + key * D + 8 * c) = vv[i];
+    }
+    if (k0 + NWV * KB < kend) load_chunk(k0 + NWV * KB);
+    // ---- online softmax of query row mi over this chunk: lane holds keys k0 + 16 kt + 4 g + v
+    float cm = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int key = k0 + kt * 16 + 4 * g + v;
+        const float sv = key < lim ? sc[kt][v] * p.scale_log2 : -INFINITY;
+        sc[kt][v] = sv;
+        cm = fmaxf(cm, sv);
+      }
+    cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+    const float nm = fmaxf(run_m, cm);
+    const float mu = nm == -INFINITY ? 0.f : nm;
+    const float alpha = run_m == -INFINITY ? 0.f : exp2f(run_m - mu);
+    float ls = 0.f;
+    uint32_t p2[4][2];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      float e[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        e[v] = exp2f(sc[kt][v] - mu);
+        ls += e[v];
+      }
+      p2[kt][0] = pack2bf(e[0], e[1]);
+      p2[kt][1] = pack2bf(e[2], e[3]);
+    }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    run_l = run_l * alpha + ls;
+    run_m = nm;
+    // rescale O rows 4 g + v by their row's alpha (held by lane 4 g + v)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float a = __shfl(alpha, 4 * g + v, 64);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) o[dt][v] *= a;
+    }
+    // ---- P as the A operand: lane (mi, h) needs P[mi][32 ks + 8 h + j], j = 0..7
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int src0 = (2 * (g & 1)) * 16 + mi, src1 = src0 + 16;
+      const bool hi = (g >> 1) != 0;
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint32_t a0 = __shfl(p2[2 * ks][q], src0, 64), b0 = __shfl(p2[2 * ks + 1][q], src0, 64);
+        const uint32_t a1 = __shfl(p2[2 * ks][q], src1, 64), b1 = __shfl(p2[2 * ks + 1][q], src1, 64);
+        w[q] = hi ? b0 : a0;
+        w[2 + q] = hi ? b1 : a1;
+      }
+      const u32x4_t pw = {w[0], w[1], w[2], w[3]};
+      const bf16x8_t pf = __builtin_bit_cast(bf16x8_t, pw);
+      // V B-fragments: keys 32 ks + 8 g + (0..3 | 4..7), columns 16 dt + 4 p of the 16-lane group
+      const int qrow = (lane & 15) >> 2, pc = lane & 3;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const uint16_t* a = vt + (32 * ks + 8 * g + qrow) * D + 16 * dt + 4 * pc;
+        const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)a);
+        const short4_t hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a + 4 * D));
+        const short8_t v8 = {lo[0], lo[1], lo[2], lo[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8_t, v8), o[dt], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- merge the 4 waves: stats of row mi from lanes g == 0, O rows 4 g + v, cols 16 dt + (lane & 15)
+  if (g == 0) {
+    red_m[wid * 16 + mi] = run_m;
+    red_l[wid * 16 + mi] = run_l;
+  }
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) red_o[(wid * 16 + 4 * g + v) * D + 16 * dt + (lane & 15)] = o[dt][v];
+  __syncthreads();
+  const int64_t pbase = ((int64_t)bh * p.nsplit + split) * M;
+  for (int it = tid; it < M * D; it += 64 * NWV) {
+    const int m = it / D, d = it % D;
+    float gm = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) gm = fmaxf(gm, red_m[w * 16 + m]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      const float mw = red_m[w * 16 + m];
+      const float wt = (mw == -INFINITY) ? 0.f : exp2f(mw - gm);
+      L += wt * red_l[w * 16 + m];
+      acc += wt * red_o[(w * 16 + m) * D + d];
+    }
+    if (p.nsplit == 1) {
+      const int tt = m / G, gg = m % G;
+      p.out[(int64_t)b * p.o_sb + (int64_t)tt * p.o_st + (int64_t)(hkv * G + gg) * p.o_sh + d] =
+          f2bf(L > 0.f ? acc / L : 0.f);
+    } else {
+      p.po[(pbase + m) * D + d] = acc;
+      if (d == 0) {
+        p.pm[pbase + m] = gm == -INFINITY ? -INFINITY : gm * 0.69314718056f;   // log2 -> natural-log domain
+        p.pl[pbase + m] = L;
+      }
+    }
+  }
+}
+
+}  // namespace dattn
+
+// Returns -1 when the shape is not covered (caller falls back to the 128-key-chunk kernel).
+int decode_attn2_launch(const void* q, const int64_t* qs, const void* kc, const void* vc, const int64_t* cs,
+                        const int* cache_idx, const int* seq_len, float* po, float* pm, float* pl, void* out,
+                        const int64_t* os, int B, int T, int Hq, int Hkv, int D, int Lmax, float scale, int* nsplit_out,
+                        hipStream_t stream) {
+  if (Hkv <= 0 || Hq % Hkv) return -1;
+  const int M = (Hq / Hkv) * T;
+  if (M > 16 || (D != 64 && D != 128)) return -1;
+  dattn::Params p;
+  p.q = (const uint16_t*)q; p.q_sb = qs[0]; p.q_st = qs[1]; p.q_sh = qs[2];
+  p.kc = (const uint16_t*)kc; p.vc = (const uint16_t*)vc;
+  p.c_sb = cs[0]; p.c_sh = cs[1]; p.c_sl = cs[2];
+  p.cache_idx = cache_idx; p.seq_len = seq_len;
+  p.out = (uint16_t*)out; p.o_sb = os[0]; p.o_st = os[1]; p.o_sh = os[2];
+  p.po = po; p.pm = pm; p.pl = pl;
+  p.B = B; p.T = T; p.Hq = Hq; p.Hkv = Hkv;
+  p.nsplit = Lmax <= dattn::KPS ? 1 : (Lmax + dattn::KPS - 1) / dattn::KPS;
+  p.scale_log2 = scale * 1.4426950408889634f;
+  *nsplit_out = p.nsplit;
+  // D = 64: 8 waves (<= 2 chunks each per 1024-key split); D = 128: 4 waves (LDS: V tiles + merge)
+  const int nwv = D == 64 ? 8 : 4;
+  const size_t lds = (size_t)nwv * dattn::KB * D * 2 + (size_t)nwv * 16 * D * 4 + (size_t)2 * nwv * 16 * 4;
+  const dim3 grid(B * Hkv * p.nsplit), block(64 * nwv);
+  if (D == 64) {
+    (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<64, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((dattn::attn_kernel<64, 8>), grid, block, lds, stream, p);
+  } else {
+    (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<128, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((dattn::attn_kernel<128, 4>), grid, block, lds, stream, p);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace nxd

@@ -1,0 +1,337 @@
+// Fused decode-step GEMVs (token generation, M <= 8 rows): each projection of a Llama layer is ONE
+// launch that also does the element-wise work around it, so a decode layer is 5 kernels instead of
+// 10 (reference: examples/inference/modules/attention/attention_base.py:141-170 and
+// model_base.py:388-422 run RMSNorm, QKV, RoPE, the KV-cache scatter, o_proj, the residual adds,
+// the MLP as separate graph ops):
+//
+//   QKV   : RMSNorm(h) prologue -> x.Wqkv^T -> RoPE on q/k (rotate-half pairs d, d + D/2 are the two
+//           rows of one wave) -> q to the output buffer, k/v straight into the KV cache at pos[m]
+//   O     : a.Wo^T with the residual add as epilogue: h[m, n] = h + bf16(acc) (in place)
+//   GATEUP: RMSNorm(h) prologue -> silu(x.Wg^T) * (x.Wu^T)   (fused gate/up weight [2N, K])
+//   DOWN  : a.Wd^T + residual add (in place), like O
+//   plain : x.W^T, optional RMSNorm prologue (final norm + lm_head)
+//
+// Decode is weight-streaming bound (every weight byte read once per token): one wave owns NW
+// weight rows and issues all of its row segments' 16-byte loads before the FMAs (4 k-steps of 512
+// elements per round), so a CU keeps ~48 KB of weight loads in flight.  The normalised activation
+// rows are built once per workgroup in LDS (the block recomputes sum(h^2) from L2: K <= 16 K
+// elements, negligible next to the weights) and read back by every wave with ds_read_b128.
+#include "common.h"
+
+namespace nxd {
+namespace dfused {
+
+enum Epi { PLAIN = 0, RESID = 1, GLU = 2, ROPE_KV = 3 };
+
+struct Params {
+  const uint16_t* x;      // [M, K] activations (row stride ldx)
+  int64_t ldx;
+  const uint16_t* norm_w; // [K] RMSNorm weight (NORM variants)
+  float eps;
+  const uint16_t* w;      // [Nw, K] weights (row stride ldw)
+  int64_t ldw;
+  uint16_t* y;            // [M, N] output (RESID: residual stream updated in place)
+  int64_t ldy;
+  int M, N, K;            // N = output columns (GLU: up rows start at N)
+  // ROPE_KV: y rows hold [nq | nkv | nkv] heads of D; k/v also go to the cache
+  int nq, nkv, D;
+  const float* cos_t;     // [max_pos, D/2]
+  const float* sin_t;
+  const int64_t* pos;     // [M] absolute position of each row
+  int T;                  // rows per sequence (cache row = cache_idx[m / T])
+  uint16_t* kc;
+  uint16_t* vc;
+  int64_t c_sb, c_sh, c_sl;
+  const int* cache_idx;   // [M / T] (nullable: identity)
+  int Lmax;
+  int max_pos;            // rows of the cos/sin tables (positions are clamped into them)
+};
+
+constexpr int U = 4;   // 512-element k-steps per load round
+
+// Workgroup = 4 waves = (4 / KS) row groups x KS k-slices: a row group's NW weight rows are split
+// over KS waves (partials reduced through LDS), so a short-N / long-K projection (o_proj, down)
+// still has thousands of waves streaming.  The first round of weight loads is issued before the
+// RMSNorm prologue: the weights do not depend on the activations.
+template <int MM, int NW, int EPI, bool NORM, int KS>
+__global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* xs = reinterpret_cast<uint16_t*>(smem);   // NORM: [MM][K] normalised bf16 rows
+  __shared__ float red[4][MM];
+  __shared__ float part[4][MM][NW];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int rg = wid / KS, ks = wid % KS;
+  const int wave = blockIdx.x * (4 / KS) + rg;          // row-group index
+
+  // ---- this row group's weight rows (clamped; inactive groups compute but never store)
+  int rows[NW];
+  bool active = true;
+  if (EPI == GLU) {   // NW / 2 (gate, up) row pairs per wave
+    active = wave * (NW / 2) < p.N;
+#pragma unroll
+    for (int i = 0; i < NW / 2; ++i) {
+      rows[2 * i] = min(wave * (NW / 2) + i, p.N - 1);
+      rows[2 * i + 1] = rows[2 * i] + p.N;
+    }
+  } else if (EPI == ROPE_KV) {
+    const int half = p.D / 2;
+    const int npair = (p.nq + p.nkv) * half;   // rotary (d, d + D/2) row pairs of the q and k heads
+    const int nv = p.nkv * p.D;                // v rows, two per wave
+    if (wave < npair) {
+      const int h = wave / half, d = wave % half;
+      rows[0] = h * p.D + d;
+      rows[1] = rows[0] + half;
+    } else {
+      const int r = (p.nq + p.nkv) * p.D + 2 * (wave - npair);
+      active = (wave - npair) * 2 < nv;
+      rows[0] = min(r, p.N - 1);
+      rows[1] = min(r + 1, p.N - 1);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NW; ++i) rows[i] = min(wave * NW + i, p.N - 1);
+    active = wave * NW < p.N;
+  }
+
+  const int kc = ((p.K + KS - 1) / KS + 7) & ~7;
+  const int kbeg = min(ks * kc, p.K), kend = min(p.K, kbeg + kc);
+  u32x4_t wv[NW][U];
+  auto load_round = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = base + lane * 8 + u * 512;
+#pragma unroll
+      for (int r = 0; r < NW; ++r)
+        wv[r][u] = k < kend ? *reinterpret_cast<const u32x4_t*>(p.w + (int64_t)rows[r] * p.ldw + k) : u32x4_t{0, 0, 0, 0};
+    }
+  };
+  load_round(kbeg);
+
+  if (NORM) {
+    float ss[MM];
+#pragma unroll
+    for (int m = 0; m < MM; ++m) ss[m] = 0.f;
+    for (int k = tid * 8; k < p.K; k += 256 * 8) {
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        if (m < p.M) {
+          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(p.x + (int64_t)m * p.ldx + k);
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss[m] += f[j] * f[j];
+          *reinterpret_cast<u32x4_t*>(xs + m * p.K + k) = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+      const float sm = wave_sum(ss[m]);
+      if (lane == 0) red[wid][m] = sm;
+    }
+    __syncthreads();
+    float rstd[MM];
+#pragma unroll
+    for (int m = 0; m < MM; ++m) rstd[m] = rsqrtf((red[0][m] + red[1][m] + red[2][m] + red[3][m]) / (float)p.K + p.eps);
+    for (int k = tid * 8; k < p.K; k += 256 * 8) {
+      float g[8];
+      unpack8(*reinterpret_cast<const u32x4_t*>(p.norm_w + k), g);
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        if (m < p.M) {
+          float f[8];
+          unpack8(*reinterpret_cast<const u32x4_t*>(xs + m * p.K + k), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = f[j] * rstd[m] * g[j];
+          *reinterpret_cast<u32x4_t*>(xs + m * p.K + k) = pack8(f);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  float acc[MM][NW];
+#pragma unroll
+  for (int m = 0; m < MM; ++m)
+#pragma unroll
+    for (int r = 0; r < NW; ++r) acc[m][r] = 0.f;
+
+  for (int base = kbeg; base < kend; base += 512 * U) {
+    if (base != kbeg) load_round(base);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = base + lane * 8 + u * 512;
+      if (k < kend) {
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+          if (m < p.M) {
+            float xf[8];
+            const uint16_t* xp = NORM ? (xs + m * p.K + k) : (p.x + (int64_t)m * p.ldx + k);
+            unpack8(*reinterpret_cast<const u32x4_t*>(xp), xf);
+#pragma unroll
+            for (int r = 0; r < NW; ++r) {
+              float wf[8];
+              unpack8(wv[r][u], wf);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) acc[m][r] += xf[e] * wf[e];
+            }
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MM; ++m)
+#pragma unroll
+    for (int r = 0; r < NW; ++r) acc[m][r] = wave_sum(acc[m][r]);
+  if (KS > 1) {
+    if (lane == 0) {
+#pragma unroll
+      for (int m = 0; m < MM; ++m)
+#pragma unroll
+        for (int r = 0; r < NW; ++r) part[wid][m][r] = acc[m][r];
+    }
+    __syncthreads();
+    if (ks != 0) return;
+#pragma unroll
+    for (int m = 0; m < MM; ++m)
+#pragma unroll
+      for (int r = 0; r < NW; ++r) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < KS; ++j) t += part[wid + j][m][r];
+        acc[m][r] = t;
+      }
+  }
+  if (lane != 0 || !active) return;
+
+#pragma unroll
+  for (int m = 0; m < MM; ++m) {
+    if (m >= p.M) continue;
+    uint16_t* yr = p.y + (int64_t)m * p.ldy;
+    if (EPI == GLU) {
+#pragma unroll
+      for (int i = 0; i < NW / 2; ++i) {
+        if (wave * (NW / 2) + i >= p.N) continue;
+        const float g = acc[m][2 * i], u = acc[m][2 * i + 1];
+        yr[rows[2 * i]] = f2bf(g / (1.f + __expf(-g)) * u);
+      }
+    } else if (EPI == ROPE_KV) {
+      const int half = p.D / 2;
+      const int64_t ps = p.pos[m];
+      const int b = m / p.T;
+      const int cb = p.cache_idx ? p.cache_idx[b] : b;
+      const bool in_cache = ps >= 0 && ps < p.Lmax;
+      const int qk_rows = (p.nq + p.nkv) * p.D;
+      if (rows[0] < qk_rows && rows[1] == rows[0] + half) {
+        const int h = rows[0] / p.D, d = rows[0] % p.D;
+        const int64_t pt = ps < 0 ? 0 : (ps >= p.max_pos ? p.max_pos - 1 : ps);
+        const float c = p.cos_t[pt * half + d], sn = p.sin_t[pt * half + d];
+        const float x1 = bf2f(f2bf(acc[m][0])), x2 = bf2f(f2bf(acc[m][1]));   // bf16 projection output
+        const uint16_t o1 = f2bf(x1 * c - x2 * sn), o2 = f2bf(x2 * c + x1 * sn);
+        yr[rows[0]] = o1;
+        yr[rows[1]] = o2;
+        if (h >= p.nq && in_cache) {
+          uint16_t* kp = p.kc + (int64_t)cb * p.c_sb + (int64_t)(h - p.nq) * p.c_sh + ps * p.c_sl;
+          kp[d] = o1;
+          kp[d + half] = o2;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          if (r == 1 && rows[1] == rows[0]) break;
+          const uint16_t o = f2bf(acc[m][r]);
+          yr[rows[r]] = o;
+          const int vr = rows[r] - qk_rows;
+          if (in_cache)
+            p.vc[(int64_t)cb * p.c_sb + (int64_t)(vr / p.D) * p.c_sh + ps * p.c_sl + vr % p.D] = o;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < NW; ++r) {
+        const int n = wave * NW + r;
+        if (n >= p.N) continue;
+        if (EPI == RESID) yr[n] = f2bf(bf2f(yr[n]) + bf2f(f2bf(acc[m][r])));
+        else yr[n] = f2bf(acc[m][r]);
+      }
+    }
+  }
+}
+
+// k-slices per row group: split K while the grid stays <= 8192 waves and slices keep >= 1024
+// elements (o_proj 2048 x 2048 -> 2, down 2048 x 8192 -> 4, gate_up / lm_head -> 1)
+int g_glu_pairs = 1;   // knob 0: (gate, up) row pairs per wave of the GLU projection (1 | 2)
+int g_ks = 0;          // knob 1: k-slices per row group (0 = pick_ks)
+
+static int pick_ks(int groups, int K) {
+  if (g_ks == 1 || g_ks == 2 || g_ks == 4) return g_ks;
+  int ks = 1;
+  while (ks < 4 && groups * ks * 2 <= 8192 && K / (ks * 2) >= 1024) ks *= 2;
+  return ks;
+}
+
+template <int MM, int NW, int EPI, bool NORM>
+static int launch(const Params& p, int groups, hipStream_t s) {
+  const size_t lds = NORM ? (size_t)MM * p.K * 2 : 0;
+  const int ks = pick_ks(groups, p.K);
+  const dim3 grid((unsigned)((groups * ks + 3) / 4)), block(256);
+  if (ks == 4)
+    hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 4>), grid, block, lds, s, p);
+  else if (ks == 2)
+    hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 2>), grid, block, lds, s, p);
+  else
+    hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 1>), grid, block, lds, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+template <int MM>
+static int dispatch(const Params& p, int epi, bool norm, hipStream_t s) {
+  switch (epi) {
+    case PLAIN: {
+      const int nw = p.N >= 16384 ? 2 : 1;
+      const int groups = (p.N + nw - 1) / nw;
+      if (nw == 2) return norm ? launch<MM, 2, PLAIN, true>(p, groups, s) : launch<MM, 2, PLAIN, false>(p, groups, s);
+      return norm ? launch<MM, 1, PLAIN, true>(p, groups, s) : launch<MM, 1, PLAIN, false>(p, groups, s);
+    }
+    case RESID:
+      return norm ? launch<MM, 1, RESID, true>(p, p.N, s) : launch<MM, 1, RESID, false>(p, p.N, s);
+    case GLU:
+      if (g_glu_pairs == 2) {
+        const int groups = (p.N + 1) / 2;
+        return norm ? launch<MM, 4, GLU, true>(p, groups, s) : launch<MM, 4, GLU, false>(p, groups, s);
+      }
+      return norm ? launch<MM, 2, GLU, true>(p, p.N, s) : launch<MM, 2, GLU, false>(p, p.N, s);
+    case ROPE_KV: {
+      const int groups = (p.nq + p.nkv) * (p.D / 2) + (p.nkv * p.D + 1) / 2;
+      return norm ? launch<MM, 2, ROPE_KV, true>(p, groups, s) : launch<MM, 2, ROPE_KV, false>(p, groups, s);
+    }
+  }
+  return -1;
+}
+
+}  // namespace dfused
+
+void dgemv_set_knob(int which, int value) {
+  if (which == 0) dfused::g_glu_pairs = value == 2 ? 2 : 1;
+  else if (which == 1) dfused::g_ks = value;
+}
+
+int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,
+                 int64_t ldy, int M, int N, int K, int nq, int nkv, int D, const float* cos_t, const float* sin_t,
+                 const int64_t* pos, int T, void* kc, void* vc, int64_t c_sb, int64_t c_sh, int64_t c_sl,
+                 const int* cache_idx, int Lmax, int max_pos, hipStream_t stream) {
+  if (M < 1 || M > 8 || N < 1 || K < 8 || (K % 8)) return -1;
+  if (norm_w && (size_t)M * K * 2 > 65536) return -2;
+  dfused::Params p{static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(norm_w), eps,
+                   static_cast<const uint16_t*>(w), ldw, static_cast<uint16_t*>(y), ldy, M, N, K, nq, nkv, D, cos_t,
+                   sin_t, pos, T, static_cast<uint16_t*>(kc), static_cast<uint16_t*>(vc), c_sb, c_sh, c_sl, cache_idx,
+                   Lmax, max_pos};
+  const bool norm = norm_w != nullptr;
+  if (M == 1) return dfused::dispatch<1>(p, epi, norm, stream);
+  if (M == 2) return dfused::dispatch<2>(p, epi, norm, stream);
+  if (M <= 4) return dfused::dispatch<4>(p, epi, norm, stream);
+  return dfused::dispatch<8>(p, epi, norm, stream);
+}
+
+}  // namespace nxd

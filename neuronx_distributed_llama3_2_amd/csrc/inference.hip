@@ -456,12 +456,39 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(const T* __restrict__
 
 }  // namespace dec
 
+int decode_attn2_launch(const void*, const int64_t*, const void*, const void*, const int64_t*, const int*, const int*,
+                        float*, float*, float*, void*, const int64_t*, int, int, int, int, int, int, float, int*, hipStream_t);
+
+static int g_attn_v2 = [] { const char* e = getenv("NXD_DECODE_ATTN_V2"); return e ? atoi(e) : 1; }();
+void decode_attn_set_v2(int v) { g_attn_v2 = v; }
+
 int decode_attn_launch(const void* q, const int64_t* qs, const void* kc, const void* vc, const int64_t* cs,
                        const int* cache_idx, const int* seq_len, float* po, float* pm, float* pl, int* counters, void* out,
                        const int64_t* os, int B, int T, int Hq, int Hkv, int D, int nsplit, float scale, hipStream_t stream) {
   using namespace dec;
   if (Hkv <= 0 || Hq % Hkv) return -1;
   const int M = (Hq / Hkv) * T;
+  // small query groups: the MFMA flash-decoding kernel (decode_attn.hip), merge only past 1024 keys
+  if (g_attn_v2) {
+    int ns2 = 0;
+    const int rc = decode_attn2_launch(q, qs, kc, vc, cs, cache_idx, seq_len, po, pm, pl, out, os, B, T, Hq, Hkv, D,
+                                       nsplit * kChunk, scale, &ns2, stream);
+    if (rc == 0 && ns2 > 1) {
+      DecodeParams mp;
+      mp.q = (const uint16_t*)q; mp.q_sb = qs[0]; mp.q_st = qs[1]; mp.q_sh = qs[2];
+      mp.kc = (const uint16_t*)kc; mp.vc = (const uint16_t*)vc;
+      mp.c_sb = cs[0]; mp.c_sh = cs[1]; mp.c_sl = cs[2];
+      mp.cache_idx = cache_idx; mp.seq_len = seq_len; mp.po = po; mp.pm = pm; mp.pl = pl;
+      mp.B = B; mp.T = T; mp.Hq = Hq; mp.Hkv = Hkv; mp.nsplit = ns2; mp.scale = scale; mp.fused_merge = 0;
+      const size_t mlds = (size_t)((M + 3) & ~3) * 4 + (size_t)4 * 8 * D * 4 + (size_t)ns2 * M * 4;
+      if (D == 64)
+        hipLaunchKernelGGL(merge_kernel<64>, dim3(B * Hkv), dim3(256), mlds, stream, mp, (uint16_t*)out, os[0], os[1], os[2]);
+      else
+        hipLaunchKernelGGL(merge_kernel<128>, dim3(B * Hkv), dim3(256), mlds, stream, mp, (uint16_t*)out, os[0], os[1], os[2]);
+      return (int)hipGetLastError();
+    }
+    if (rc != -1) return rc;   // -1: shape not covered by the MFMA kernel
+  }
   DecodeParams p;
   p.q = (const uint16_t*)q; p.q_sb = qs[0]; p.q_st = qs[1]; p.q_sh = qs[2];
   p.kc = (const uint16_t*)kc; p.vc = (const uint16_t*)vc;

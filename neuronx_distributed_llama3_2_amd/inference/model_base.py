@@ -10,6 +10,11 @@
   kernel (inference.hip) reading the KV cache up to a per-sequence DEVICE length, so a decode
   step has static shapes and no host sync — it is captured into hipGraphs (inference/graphs.py).
 
+Decode fast path (TP = 1, bf16 weights, <= 8 new tokens): each projection is one fused GEMV
+(csrc/decode_fused.hip) that also does the surrounding element-wise work -- RMSNorm prologues,
+RoPE + KV-cache write after QKV, residual adds after o_proj / down -- so a layer is 5 launches
+(QKV, attention, o_proj, gate_up, down) instead of 10 (`NXD_DECODE_FUSED=0` disables it).
+
 KV cache: ONE allocation [layers, 2, max_batch, kv_heads_local, max_len, head_dim] (bf16);
 `seq_ids` selects cache rows (continuous batching).
 """
@@ -17,6 +22,7 @@ KV cache: ONE allocation [layers, 2, max_batch, kv_heads_local, max_len, head_di
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -85,6 +91,8 @@ class DecoderInferenceMixin:
         prefill=True: the new tokens start at position 0 (causal flash attention over them)."""
         assert self.kv_cache is not None, "call setup_kv_cache() first"
         B, T = input_ids.shape
+        if not prefill and self._decode_fusable(input_ids):
+            return self._forward_decode_fused(input_ids, positions, seq_ids, cache_len, last_index, return_hidden)
         nq, nkv, D = self.nq, self.nkv, self.head_dim
         W = (nq + 2 * nkv) * D
         cos_t, sin_t = self.model.rope_cache.tables(input_ids.device)
@@ -119,6 +127,78 @@ class DecoderInferenceMixin:
         h, _ = self._norm(x, self.model.norm.weight, residual)
         logits = self._gather_vocab(self._proj(self.lm_head, h))
         return (logits, h) if return_hidden else logits
+
+    # ------------------------------------------------------------------ fused decode path
+    def _fused_ffn_weights(self, layer):
+        """(post-attention norm weight, fused gate/up [2I, H], down [H, I]) when the feed-forward
+        block is a dense bias-free SwiGLU MLP the fused decode kernels can run, else None."""
+        return None
+
+    def _decode_fusable(self, input_ids: torch.Tensor) -> bool:
+        ok = getattr(self, "_decode_fused_ok", None)
+        if ok is None:
+            ok = self._check_decode_fusable()
+            self._decode_fused_ok = ok
+        M = input_ids.numel()
+        return ok and input_ids.is_cuda and M <= 8 and M * self.config.hidden_size <= 32768
+
+    def _check_decode_fusable(self) -> bool:
+        if os.environ.get("NXD_DECODE_FUSED", "1") == "0" or self.tp != 1:
+            return False
+        if type(self)._qkv_hook is not DecoderInferenceMixin._qkv_hook or type(self)._norm is not DecoderInferenceMixin._norm:
+            return False
+        if self.head_dim % 2 or self.head_dim > 256:
+            return False
+        for layer in self.model.layers:
+            attn = layer.self_attn
+            w, b = attn.qkv_proj._fused_weight_bias() if hasattr(attn.qkv_proj, "_fused_weight_bias") \
+                else (attn.qkv_proj.weight, getattr(attn.qkv_proj, "bias", None))
+            if b is not None or w.dtype != torch.bfloat16 or getattr(attn.o_proj, "bias", None) is not None:
+                return False
+            if attn.o_proj.weight.dtype != torch.bfloat16 or self._fused_ffn_weights(layer) is None:
+                return False
+        lm = self.lm_head.weight
+        return lm.dtype == torch.bfloat16 and getattr(self.lm_head, "bias", None) is None
+
+    def _forward_decode_fused(self, input_ids, positions, seq_ids, cache_len, last_index, return_hidden):
+        C = ops.ext()
+        B, T = input_ids.shape
+        M = B * T
+        nq, nkv, D = self.nq, self.nkv, self.head_dim
+        W = (nq + 2 * nkv) * D
+        cos_t, sin_t = self.model.rope_cache.tables(input_ids.device)
+        pos = positions.reshape(-1).to(torch.int64).contiguous()
+        sid32 = seq_ids.to(torch.int32).contiguous() if seq_ids is not None else None
+        emb = self.model.embed_tokens
+        res = ops.vocab_parallel_embedding(input_ids, emb.weight, emb.start_index).reshape(M, -1).contiguous()
+        qkv = torch.empty((M, W), dtype=res.dtype, device=res.device)
+        for i, layer in enumerate(self.model.layers):
+            attn = layer.self_attn
+            w_qkv = attn.qkv_proj._fused_weight_bias()[0] if hasattr(attn.qkv_proj, "_fused_weight_bias") \
+                else attn.qkv_proj.weight
+            kc, vc = self.kv_cache[i, 0], self.kv_cache[i, 1]
+            # RMSNorm -> QKV -> RoPE -> k/v into the cache, one launch
+            C.dgemv(3, res, layer.input_layernorm.weight, self.eps, w_qkv, qkv, nq, nkv, D, cos_t, sin_t, pos, T,
+                    kc, vc, sid32)
+            q = qkv.view(B, T, nq + 2 * nkv, D)[:, :, :nq]
+            o = ops.decode_attention(q, kc, vc, cache_len, sid32)
+            C.dgemv(1, o.reshape(M, nq * D), None, 0.0, attn.o_proj.weight, res, 0, 0, 0, None, None, None, 1,
+                    None, None, None)                                   # res += o_proj(o)
+            ln2, w_gu, w_d = self._fused_ffn_weights(layer)
+            a = torch.empty((M, w_d.shape[1]), dtype=res.dtype, device=res.device)
+            C.dgemv(2, res, ln2, self.eps, w_gu, a, 0, 0, 0, None, None, None, 1, None, None, None)  # norm+SwiGLU
+            C.dgemv(1, a, None, 0.0, w_d, res, 0, 0, 0, None, None, None, 1, None, None, None)   # res += down(a)
+        h = res.view(B, T, -1)
+        if last_index is not None:
+            h = h[torch.arange(B, device=h.device), last_index]
+        h2 = h.reshape(-1, h.shape[-1]).contiguous()
+        logits = torch.empty((h2.shape[0], self.lm_head.weight.shape[0]), dtype=res.dtype, device=res.device)
+        C.dgemv(0, h2, self.model.norm.weight, self.eps, self.lm_head.weight, logits, 0, 0, 0, None, None, None, 1,
+                None, None, None)                                       # final norm + lm_head
+        logits = logits.view(h.shape[:-1] + (logits.shape[-1],))
+        if return_hidden:
+            return logits, ops.rms_norm(h, self.model.norm.weight, self.eps)[0]
+        return logits
 
     @torch.no_grad()
     def forward_tree(self, tokens: torch.Tensor, positions: torch.Tensor, tree_mask: torch.Tensor, prefix_len: int,

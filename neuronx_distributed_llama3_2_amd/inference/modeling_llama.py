@@ -24,6 +24,14 @@ class LlamaInferenceModel(DecoderInferenceMixin, LlamaForCausalLM):
         LlamaForCausalLM.__init__(self, cfg, dtype=dtype, device=device)
         self._init_inference(config)
 
+    def _fused_ffn_weights(self, layer):
+        mlp = layer.mlp
+        w_gu, w_d = mlp.gate_up_proj.weight, mlp.down_proj.weight
+        if w_gu.dtype != torch.bfloat16 or w_d.dtype != torch.bfloat16 or \
+                getattr(mlp.gate_up_proj, "bias", None) is not None or getattr(mlp.down_proj, "bias", None) is not None:
+            return None
+        return layer.post_attention_layernorm.weight, w_gu, w_d
+
     def _ffn(self, layer, h: torch.Tensor) -> torch.Tensor:
         mlp = layer.mlp
         a = self._proj(mlp.gate_up_proj, h, glu=True)   # SwiGLU fused into the decode GEMV

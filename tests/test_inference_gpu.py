@@ -184,3 +184,37 @@ def test_mixtral_inference_gpu_graphs_match_cpu():
     # same kernels; hipBLASLt stream-K prefill GEMMs may reorder fp32 sums run to run (see
     # test_graph_decode_matches_eager), so allow a late near-tie flip
     assert torch.equal(a[:, :46], b[:, :46]) and (a == b).float().mean() > 0.9, (a, b)
+
+
+@pytest.mark.parametrize("hidden,heads", [(512, 8), (1024, 8)])   # head_dim 64 and 128
+def test_fused_decode_matches_unfused(hidden, heads):
+    """decode_fused.hip path (norm / RoPE / KV write / residual fused into the GEMVs) vs the
+    unfused kernel chain: same greedy tokens, same KV cache, close logits."""
+    from transformers import LlamaConfig, LlamaForCausalLM as HF
+
+    cfg = LlamaConfig(hidden_size=hidden, intermediate_size=2 * hidden, num_hidden_layers=2, num_attention_heads=heads,
+                      num_key_value_heads=2, vocab_size=1000, max_position_embeddings=1024, rms_norm_eps=1e-5,
+                      rope_theta=500000.0, tie_word_embeddings=True, eos_token_id=2)
+    torch.manual_seed(0)
+    sd = {k: v.detach().clone() for k, v in HF(cfg).state_dict().items()}
+    f = _model(cfg, sd, torch.bfloat16, graphs=False, steps=1, device=torch.device("cuda"))
+    u = _model(cfg, sd, torch.bfloat16, graphs=False, steps=1, device=torch.device("cuda"))
+    u.model._decode_fused_ok = False
+    torch.manual_seed(5)
+    ids = torch.randint(3, cfg.vocab_size, (2, 33))
+    a = f.generate(ids, max_new_tokens=24, eos_token_id=-1)
+    assert f.model._decode_fused_ok is True, "fused decode path was not taken"
+    b = u.generate(ids, max_new_tokens=24, eos_token_id=-1)
+    assert torch.equal(a[:, :43].cpu(), b[:, :43].cpu())
+    assert (a.cpu() == b.cpu()).float().mean() > 0.9
+    kf, ku = f.model.kv_cache[:, :, :, :, :50].float(), u.model.kv_cache[:, :, :, :, :50].float()
+    assert ((kf - ku).abs().max() / ku.abs().max()).item() < 3e-2
+    # one decode step on identical caches: logits agree
+    f.model.kv_cache.copy_(u.model.kv_cache)
+    last = b[:, -1:].cuda()
+    pos = torch.full((2, 1), b.shape[1] - 1, dtype=torch.int64, device="cuda")
+    sid = torch.arange(2, device="cuda")
+    clen = torch.full((2,), b.shape[1], dtype=torch.int32, device="cuda")
+    lf = f.model.forward_tokens(last, pos, sid, clen).float()
+    lu = u.model.forward_tokens(last, pos, sid, clen).float()
+    assert ((lf - lu).abs().max() / lu.abs().max()).item() < 3e-2

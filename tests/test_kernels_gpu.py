@@ -389,3 +389,26 @@ def test_wgrad_accumulate_layouts(mode, monkeypatch):
         gemm.wgrad_accumulate_(mg, go, x)
         ref += go.float().t() @ x.float()
     assert _rel(mg, ref) < 1e-3
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("Hq,Hkv,T", [(32, 8, 1), (8, 1, 2), (64, 8, 2), (16, 2, 1)])
+@pytest.mark.parametrize("L", [384, 1024, 5000])
+def test_decode_attention_mfma_groups(D, Hq, Hkv, T, L):
+    """MFMA flash-decoding kernel (decode_attn.hip, M = Hq/Hkv * T <= 16): one split up to 1024 keys,
+    split + merge beyond; ragged lengths incl. a single visible key and chunk-boundary lengths."""
+    B = 4
+    torch.manual_seed(2)
+    kc = torch.randn(B, Hkv, L, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn(B, Hkv, L, D, device=DEV, dtype=torch.bfloat16)
+    seq = torch.tensor([L, max(T, 1), min(L, 64 + T), max(T, L // 2 + 17)], device=DEV, dtype=torch.int32)
+    q = torch.randn(B, T, Hq, D, device=DEV, dtype=torch.bfloat16) * 2
+    o = ops.decode_attention(q, kc, vc, seq)
+    ro = ops.decode_attention(q.cpu(), kc.cpu(), vc.cpu(), seq.cpu())
+    assert torch.isfinite(o.float()).all()
+    assert _rel(o.cpu(), ro) < 2e-2
+    # cache rows through cache_idx (continuous batching)
+    idx = torch.tensor([3, 0, 2, 1], device=DEV, dtype=torch.int32)
+    o2 = ops.decode_attention(q, kc, vc, seq, idx)
+    ro2 = ops.decode_attention(q.cpu(), kc.cpu(), vc.cpu(), seq.cpu(), idx.cpu())
+    assert _rel(o2.cpu(), ro2) < 2e-2
