@@ -72,14 +72,16 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
             by_kind = defaultdict(list)
             index_of = {}
             for pi, p in enumerate(g["params"]):
-                if p.requires_grad:
-                    by_kind[(param_kind(p, sp_reduce), p.dtype, p.device)].append(p)
+                if p.requires_grad:   # expert-parallel params get their own (EDP-reduced) buffers
+                    by_kind[(param_kind(p, sp_reduce), p.dtype, p.device,
+                             bool(getattr(p, "expert_model_parallel", False)))].append(p)
                     index_of[id(p)] = pi
-            for (kind, _, _), plist in by_kind.items():
-                group = self.dp_group
+            for (kind, _, _, is_ep), plist in by_kind.items():
+                group, avg = self.dp_group, None
                 if any(getattr(p, "expert_model_parallel", False) for p in plist) and ps.model_parallel_is_initialized():
-                    group = ps.get_expert_data_parallel_group()
-                buf = FlatBuffer(plist, dp_group=group, zero1=zero1, shared_ids=shared, name=f"g{gi}:{kind}")
+                    group, avg = ps.get_expert_data_parallel_group(), ps.get_data_parallel_size()
+                buf = FlatBuffer(plist, dp_group=group, zero1=zero1, shared_ids=shared, name=f"g{gi}:{kind}" + (":ep" if is_ep else ""),
+                                 avg_world=avg)
                 buf.kind = kind
                 st = _BufferState(buf, g)
                 st.group_index = gi

@@ -48,11 +48,14 @@ class _GenericZero1(torch.optim.Optimizer):
             if not plist:
                 continue
             kinds = {}
-            for p in plist:
-                kinds.setdefault(param_kind(p), []).append(p)
+            for p in plist:   # expert-parallel params get their own (EDP-sharded) buffers
+                kinds.setdefault((param_kind(p), bool(getattr(p, "expert_model_parallel", False))), []).append(p)
             for kind, ps_ in kinds.items():
-                buf = FlatBuffer(ps_, dp_group=self.dp_group, zero1=True, name=kind)
-                buf.kind = kind
+                group, avg = self.dp_group, None
+                if any(getattr(p, "expert_model_parallel", False) for p in ps_) and ps.model_parallel_is_initialized():
+                    group, avg = ps.get_expert_data_parallel_group(), ps.get_data_parallel_size()
+                buf = FlatBuffer(ps_, dp_group=group, zero1=True, name=kind, avg_world=avg)
+                buf.kind = kind[0]
                 masters = []
                 for s, e in buf.shard_ranges():
                     m = torch.nn.Parameter(buf.param_data[s:e].detach().float().clone())

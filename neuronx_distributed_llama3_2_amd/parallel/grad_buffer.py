@@ -89,13 +89,19 @@ class FlatBuffer:
     ALIGN = 16  # elements
 
     def __init__(self, params: Sequence[torch.nn.Parameter], dp_group=None, zero1: bool = False,
-                 grad_dtype: torch.dtype = torch.float32, shared_ids: Optional[set] = None, name: str = ""):
+                 grad_dtype: torch.dtype = torch.float32, shared_ids: Optional[set] = None, name: str = "",
+                 avg_world: Optional[int] = None):
         self.params = list(params)
         self.name = name
         self.dp_group = dp_group
         self.dp = dist.get_world_size(group=dp_group) if (dp_group is not None and dist.is_initialized()) else 1
         self.dp_rank = dist.get_rank(group=dp_group) if (dp_group is not None and dist.is_initialized()) else 0
         self.zero1 = zero1 and self.dp > 1
+        # gradients are averaged over `avg_world` data-parallel replicas (default: the reduction
+        # group).  Expert-parallel buffers reduce over the expert-data-parallel group but average over
+        # the whole DP world: every EP rank's tokens reached the expert through the all-to-all
+        # (reference NeuronEPZero1Optimizer scales EP grads by 1 / EP after the EDP reduction).
+        self.avg_world = avg_world if avg_world is not None else self.dp
         shared_ids = shared_ids or set()
         assert self.params, "empty parameter list"
         dev = self.params[0].device
@@ -169,6 +175,8 @@ class FlatBuffer:
         """Launch any bucket not yet launched, wait for all, average over DP."""
         self.sync_enabled = False
         if self.dp == 1:
+            if average and self.avg_world > 1:
+                self.grad_data.div_(self.avg_world)
             return
         for b in self.buckets:
             if b.handle is None:
@@ -179,9 +187,9 @@ class FlatBuffer:
             b.pending = set(id(p) for p in b.params)
             if average:
                 if self.zero1:
-                    b.out.div_(self.dp)
+                    b.out.div_(self.avg_world)
                 else:
-                    self.grad_data[b.start:b.end].div_(self.dp)
+                    self.grad_data[b.start:b.end].div_(self.avg_world)
         comm.assert_no_pending_collectives("finish_grad_sync")
 
     # ---------------------------------------------------------------- ZeRO-1 views

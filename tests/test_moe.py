@@ -243,3 +243,18 @@ def test_mixtral_ep2_edp2_checkpoint_resume():
     assert len(res) == 3
     for x, y in zip(full[3:], res):
         assert abs(x - y) < 1e-5, (full, res)
+
+
+def test_mixtral_ep2_matches_ep1_training():
+    """Expert gradients are averaged over the WHOLE data-parallel world (EP x EDP ranks), not only
+    the expert-data-parallel replicas (reference NeuronEPZero1Optimizer scales EP grads by 1/EP):
+    EP=2 (2 ranks, full capacity) reproduces the single-rank loss curve, like DP=2 does."""
+    d = tempfile.mkdtemp()
+    run_distributed(_w_mixtral, 1, 1, 1, False, 2.0, os.path.join(d, "a.pt"))
+    run_distributed(_w_mixtral, 2, 1, 1, False, 2.0, os.path.join(d, "dp.pt"))
+    run_distributed(_w_mixtral, 2, 1, 2, False, 2.0, os.path.join(d, "ep.pt"))
+    a, dp, ep = (torch.load(os.path.join(d, f)) for f in ("a.pt", "dp.pt", "ep.pt"))
+    for x, y, z in zip(a, dp, ep):
+        # DP splits the router's load-balancing statistics per rank: not bit-identical to DP=1
+        assert abs(x - y) < 1e-3 * abs(x), (a, dp)
+        assert abs(y - z) < 1e-4 * abs(y), (dp, ep)
