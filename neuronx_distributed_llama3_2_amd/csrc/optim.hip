@@ -68,7 +68,27 @@ __global__ void __launch_bounds__(256) final_kernel(const float* __restrict__ pa
 
 struct AdamHyper {
   float lr, beta1, beta2, eps, wd, bc1, bc2;  // bc = 1 - beta^t
+  uint32_t sr_seed;                           // != 0: stochastic rounding of the bf16 copy-out
 };
+
+// Stochastic rounding fp32 -> bf16 (reference: NEURON_RT_STOCHASTIC_ROUNDING_EN for the bf16
+// weights): add 16 uniform random bits below the bf16 mantissa, then truncate, so an update smaller
+// than half a bf16 ulp still moves the weight with the right probability.  Counter-based hash of
+// (seed, element index): no RNG state, identical on every replica of a parameter.
+__device__ __forceinline__ uint32_t sr_hash(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint16_t f2bf_sr(float f, uint32_t seed, int64_t idx) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return f2bf(f);   // inf / nan: round as usual
+  const uint32_t r = sr_hash((uint32_t)idx * 0x9E3779B1u ^ (uint32_t)(idx >> 32) ^ seed) & 0xffffu;
+  return (uint16_t)((u + r) >> 16);
+}
 
 template <bool GBF16, bool HAS_OUT>
 __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const void* __restrict__ g, float* __restrict__ m,
@@ -98,8 +118,14 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
     *reinterpret_cast<f32x4_t*>(v + i * 4) = vv;
     if constexpr (HAS_OUT) {
       u32x2_t o;
-      o[0] = pack2bf(pv[0], pv[1]);
-      o[1] = pack2bf(pv[2], pv[3]);
+      if (h.sr_seed) {
+        const int64_t e = i * 4;
+        o[0] = (uint32_t)f2bf_sr(pv[0], h.sr_seed, e) | ((uint32_t)f2bf_sr(pv[1], h.sr_seed, e + 1) << 16);
+        o[1] = (uint32_t)f2bf_sr(pv[2], h.sr_seed, e + 2) | ((uint32_t)f2bf_sr(pv[3], h.sr_seed, e + 3) << 16);
+      } else {
+        o[0] = pack2bf(pv[0], pv[1]);
+        o[1] = pack2bf(pv[2], pv[3]);
+      }
       *reinterpret_cast<u32x2_t*>(p16 + i * 4) = o;
     }
   }
@@ -109,7 +135,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
       m[i] = h.beta1 * m[i] + (1.f - h.beta1) * gr;
       v[i] = h.beta2 * v[i] + (1.f - h.beta2) * gr * gr;
       p[i] = p[i] * decay - step * m[i] / (sqrtf(v[i]) * rbc2 + h.eps);
-      if constexpr (HAS_OUT) p16[i] = f2bf(p[i]);
+      if constexpr (HAS_OUT) p16[i] = h.sr_seed ? f2bf_sr(p[i], h.sr_seed, i) : f2bf(p[i]);
     }
 }
 
@@ -148,10 +174,10 @@ int flat_reduce_launch(const void* x, int is_bf16, int64_t n, int mode, float* p
 
 int adamw_flat_launch(float* p, const void* g, int g_is_bf16, float* m, float* v, void* p16, int64_t n, float lr, float beta1,
                       float beta2, float eps, float wd, float bc1, float bc2, const float* gscale_ptr, float gscale_host,
-                      hipStream_t stream) {
+                      uint32_t sr_seed, hipStream_t stream) {
   using namespace optim;
   if (n == 0) return 0;
-  AdamHyper h{lr, beta1, beta2, eps, wd, bc1, bc2};
+  AdamHyper h{lr, beta1, beta2, eps, wd, bc1, bc2, sr_seed};
   const int grid = grid_for(n / 4);
 #define AK(B, O) hipLaunchKernelGGL((adamw_kernel<B, O>), dim3(grid), dim3(256), 0, stream, p, g, m, v, (uint16_t*)p16, n, h, gscale_ptr, gscale_host)
   if (g_is_bf16) { if (p16) AK(true, true); else AK(true, false); }

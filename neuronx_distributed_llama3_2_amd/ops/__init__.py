@@ -9,5 +9,6 @@ from .embedding import vocab_parallel_embedding  # noqa: F401
 from .grouped_gemm import grouped_linear, grouped_linear_reference, moe_permutation  # noqa: F401
 from .flash_attn import attention_reference, flash_attn_func, flash_attn_fwd_lse, rope_attention  # noqa: F401
 from .norm import rms_norm, rms_norm_reference  # noqa: F401
-from .optim import adamw_flat_, clip_coefficient, flat_absmax, flat_sumsq, scale_flat_  # noqa: F401
+from .optim import (adamw_flat_, clip_coefficient, flat_absmax, flat_sumsq, scale_flat_, sr_seed_for_step,  # noqa: F401
+                    stochastic_round_bf16)
 from .rope import apply_rotary_reference, inv_freq_from_config, llama3_inv_freq, rope_inplace_, rope_tables  # noqa: F401

@@ -17,6 +17,7 @@ src/neuronx_distributed/utils/adamw_fp32_optim_params.py:31-155):
 from __future__ import annotations
 
 import math
+import os
 from collections import defaultdict
 from typing import Any, Dict, Iterable, List, Optional
 
@@ -54,7 +55,8 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  zero1: bool = False, dp_group=None, grad_clipping: bool = True, max_grad_norm: float = 1.0,
-                 shared_param_ids: Optional[set] = None, sp_reduce: bool = True, bias_correction: bool = True):
+                 shared_param_ids: Optional[set] = None, sp_reduce: bool = True, bias_correction: bool = True,
+                 stochastic_rounding: Optional[bool] = None):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         if dp_group is None and ps.model_parallel_is_initialized():
@@ -64,6 +66,11 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
         self.grad_clipping = grad_clipping
         self.max_grad_norm = max_grad_norm
         self.bias_correction = bias_correction
+        # stochastic rounding of the bf16 weight copy-out (reference: NEURON_RT_STOCHASTIC_ROUNDING_EN)
+        if stochastic_rounding is None:
+            env = os.environ.get("NXD_STOCHASTIC_ROUNDING", os.environ.get("NEURON_RT_STOCHASTIC_ROUNDING_EN", "0"))
+            stochastic_rounding = env == "1"
+        self.stochastic_rounding = stochastic_rounding
         self.step_count = 0
         self.grad_norm: Optional[torch.Tensor] = None
         self.buffers: List[_BufferState] = []
@@ -144,14 +151,16 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
             coef = ops.clip_coefficient(sq, self.max_grad_norm, is_sumsq=True)
             self.grad_norm = coef[1]
         self.step_count += 1
-        for b in self.buffers:
+        seed = ops.sr_seed_for_step(self.step_count) if self.stochastic_rounding else 0
+        for bi, b in enumerate(self.buffers):
             g = b.group
             beta1, beta2 = g["betas"]
             for (s, e, lo) in b.local:
                 n = e - s
                 ops.adamw_flat_(b.master[lo:lo + n], b.buf.grad_data[s:e], b.exp_avg[lo:lo + n], b.exp_avg_sq[lo:lo + n],
                                 b.buf.param_data[s:e], g["lr"], beta1, beta2, g["eps"], g["weight_decay"], self.step_count,
-                                grad_scale=coef, bias_correction=self.bias_correction)
+                                grad_scale=coef, bias_correction=self.bias_correction,
+                                sr_seed=(((seed ^ (bi * 0x9E3779B1 + s)) & 0xFFFFFFFF) or 1) if seed else 0)
         for b in self.buffers:
             b.buf.gather_params()
         return loss

@@ -151,7 +151,93 @@ def NeuronZero1Optimizer(params, optimizer_class=torch.optim.AdamW, grad_clippin
     return opt
 
 
-def NeuronEPZero1Optimizer(params, optimizer_class=torch.optim.AdamW, **kwargs):
-    """Expert-parallel ZeRO-1: expert params are sharded over the expert-data-parallel group and
-    dense params over the full DP group (handled per buffer by the flat optimizer)."""
-    return NeuronZero1Optimizer(params, optimizer_class, **kwargs)
+class _FlatEPZero1(FlatMixedPrecisionAdamW):
+    """AdamW-family ZeRO-1 with expert parallelism (reference NeuronEPZero1Optimizer,
+    optimizer/zero_redundancy_optimizer.py:158-362): dense parameters are sharded over the DP group,
+    expert parameters over the expert-data-parallel group (their own flat buffers, gradients averaged
+    over the whole DP world); ONE gradient norm over both (every shard counted once) clips both.
+
+    state_dict() has the reference's combined layout: the dense optimizer's entries first, the expert
+    optimizer's after them at `ep_param_id_offset` / `ep_param_group_offset` / `ep_base_state_offset`
+    / `ep_shape_info_offset`; `base_state` holds the flat fp32 master / moment shards of each buffer,
+    `shape_info` the parameter shapes, `state` the per-parameter step."""
+
+    def _split(self):
+        dense = [b for b in self.buffers if not b.buf.name.endswith(":ep")]
+        expert = [b for b in self.buffers if b.buf.name.endswith(":ep")]
+        return dense, expert
+
+    def state_dict(self) -> Dict[str, Any]:
+        flat = super().state_dict()
+        dense, expert = self._split()
+        bufs = {id(b): sb for b, sb in zip(self.buffers, flat["buffers"])}
+        n_groups = len(flat["param_groups"])
+
+        def part(blist, pid0, bid0, goff):
+            state, base, shapes = {}, {}, {}
+            pid = pid0
+            for i, b in enumerate(blist):
+                sb = dict(bufs[id(b)])
+                sb["layout"] = [(gi + goff, pi, off, n, shp) for (gi, pi, off, n, shp) in sb["layout"]]
+                base[bid0 + i] = sb
+                for (_, _, _, _, shp) in sb["layout"]:
+                    shapes[pid] = shp
+                    state[pid] = {"step": flat["step"]}
+                    pid += 1
+            return state, base, shapes
+
+        d_state, d_base, d_shapes = part(dense, 0, 0, 0)
+        ep_pid = len(d_shapes)
+        e_state, e_base, e_shapes = part(expert, ep_pid, len(dense), n_groups)
+        return {
+            "ep_param_id_offset": max(ep_pid, 1) if not d_shapes else ep_pid,
+            "ep_param_group_offset": n_groups,
+            "ep_base_state_offset": len(dense),
+            "ep_shape_info_offset": ep_pid,
+            "param_groups": flat["param_groups"] + flat["param_groups"],
+            "state": {**d_state, **e_state},
+            "base_state": {**d_base, **e_base},
+            "shape_info": {**d_shapes, **e_shapes},
+            "step": flat["step"],
+            "zero1": flat["zero1"],
+        }
+
+    def load_state_dict(self, sd: Dict[str, Any]) -> None:
+        if sd.get("flat_optimizer") or sd.get("flat_optimizer_full"):
+            return super().load_state_dict(sd)
+        keys = ("ep_param_id_offset", "ep_param_group_offset", "ep_base_state_offset", "ep_shape_info_offset")
+        if any(k not in sd for k in keys):
+            raise ValueError("state_dict is not compatible with expert parallelism and Zero-1.")
+        goff, boff = int(sd["ep_param_group_offset"]), int(sd["ep_base_state_offset"])
+        dense, expert = self._split()
+        base = sd["base_state"]
+        by_buf = {}
+        for i, b in enumerate(dense):
+            by_buf[id(b)] = base[i]
+        for i, b in enumerate(expert):
+            sb = dict(base[boff + i])
+            sb["layout"] = [(gi - goff, pi, off, n, shp) for (gi, pi, off, n, shp) in sb["layout"]]
+            by_buf[id(b)] = sb
+        flat = {"flat_optimizer": True, "step": int(sd["step"]), "param_groups": sd["param_groups"][:goff],
+                "buffers": [by_buf[id(b)] for b in self.buffers], "zero1": sd.get("zero1", True)}
+        super().load_state_dict(flat)
+
+
+def NeuronEPZero1Optimizer(params, optimizer_class=torch.optim.AdamW, grad_clipping: bool = True,
+                           max_norm: float = 1.0, sharding_groups=None, shared_param_ids: Optional[set] = None,
+                           save_master_weights: bool = False, **kwargs):
+    """Expert-parallel ZeRO-1: expert params sharded over the expert-data-parallel group, dense params
+    over the DP group, one combined gradient norm, reference-layout merged state dict."""
+    if sharding_groups is not None and not isinstance(sharding_groups, torch.distributed.ProcessGroup) and \
+            ps.model_parallel_is_initialized() and sharding_groups != ps.get_data_parallel_group(as_list=True):
+        raise ValueError("Custom sharding group for Zero-1 with expert parallelism is not supported.")
+    if not _is_adam_family(optimizer_class):
+        return NeuronZero1Optimizer(params, optimizer_class, grad_clipping=grad_clipping, max_norm=max_norm,
+                                    shared_param_ids=shared_param_ids, save_master_weights=save_master_weights,
+                                    **kwargs)
+    kw = {k: v for k, v in kwargs.items() if k in ("lr", "betas", "eps", "weight_decay")}
+    dp_group = ps.get_data_parallel_group() if ps.model_parallel_is_initialized() else None
+    opt = _FlatEPZero1(params, zero1=True, dp_group=dp_group, grad_clipping=grad_clipping, max_grad_norm=max_norm,
+                       shared_param_ids=shared_param_ids, **kw)
+    opt.save_master_weights = save_master_weights
+    return opt

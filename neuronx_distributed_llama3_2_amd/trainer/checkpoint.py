@@ -25,7 +25,9 @@ import torch
 import torch.distributed as dist
 
 from ..parallel_layers.parallel_state import (
+    get_data_parallel_group,
     get_data_parallel_rank,
+    get_expert_data_parallel_group,
     get_expert_data_parallel_rank,
     get_expert_model_parallel_rank,
     get_expert_model_parallel_size,
@@ -36,7 +38,7 @@ from ..parallel_layers.parallel_state import (
 from ..parallel_layers.utils import move_all_tensor_to_cpu
 from ..utils.logger import get_logger
 from ..utils.resilience import fault_point
-from ..utils.serialization import xser_load, xser_save
+from ..utils.serialization import assign_tensors_to_bins, xser_load, xser_load_info, xser_save, xser_tensors
 from .checkpoint_storage import BaseCheckpointStorage, FilesysCheckpointStorage, create_checkpoint_storage
 
 logger = get_logger()
@@ -100,6 +102,47 @@ def _snapshot(data: Any) -> Any:
     return data
 
 
+def _snapshot_owned(data: Any, owned: set, counter: List[int]) -> Any:
+    """Like _snapshot, but tensors whose xser tid (traversal index) is not in `owned` become meta
+    placeholders of the same shape / dtype / EP flag (another replica writes their files)."""
+    if isinstance(data, torch.Tensor):
+        tid = counter[0]
+        counter[0] += 1
+        if tid in owned:
+            out = _snapshot(data)
+        else:
+            out = torch.empty(data.shape, dtype=data.dtype, device="meta")
+        if getattr(data, "expert_model_parallel", False):
+            out.expert_model_parallel = True
+        return out
+    if isinstance(data, dict):
+        return {k: _snapshot_owned(v, owned, counter) for k, v in data.items()}
+    if isinstance(data, list):
+        return [_snapshot_owned(v, owned, counter) for v in data]
+    if isinstance(data, tuple):
+        return tuple(_snapshot_owned(v, owned, counter) for v in data)
+    return data
+
+
+def _model_replica_group():
+    """(group, size, rank) of the ranks holding identical copies of this rank's model shard: the
+    expert-data-parallel group under EP, else the DP group."""
+    if not (model_parallel_is_initialized() and dist.is_available() and dist.is_initialized()):
+        return None, 1, 0
+    g = get_expert_data_parallel_group() if get_expert_model_parallel_size() > 1 else get_data_parallel_group()
+    return g, dist.get_world_size(group=g), dist.get_rank(group=g)
+
+
+def _tag_expert_tensors(model, sd: Dict[str, Any]) -> None:
+    """Mark expert-parallel entries of a model state dict (recorded in xser `.info.pt`)."""
+    target = getattr(model, "module", model)
+    if not hasattr(target, "named_parameters"):
+        return
+    for n, p in target.named_parameters():
+        if getattr(p, "expert_model_parallel", False) and isinstance(sd.get(n), torch.Tensor):
+            sd[n].expert_model_parallel = True
+
+
 class CheckpointIOState:
     """Tracks the in-flight (possibly asynchronous) checkpoint and its save tasks."""
 
@@ -126,15 +169,20 @@ class CheckpointIOState:
         _barrier()
         self.tasks = []
 
-    def add_save_task(self, obj: Any, filename: str, xser: bool = False) -> None:
-        self.tasks.append((_snapshot(obj) if self.async_save else move_all_tensor_to_cpu(obj), filename, xser))
+    def add_save_task(self, obj: Any, filename: str, xser: bool = False, xser_ids=None, xser_ref: bool = True) -> None:
+        if xser_ids is not None:
+            # this rank stores only its bin of the shard's tensor files: copy just those to the host
+            snap = _snapshot_owned(obj, set(xser_ids), [0])
+        else:
+            snap = _snapshot(obj) if self.async_save else move_all_tensor_to_cpu(obj)
+        self.tasks.append((snap, filename, (xser, xser_ids, xser_ref)))
 
     def _run(self, tasks, storage):
-        for obj, fn, xser in tasks:
+        for obj, fn, (xser, ids, ref) in tasks:
             if xser and isinstance(storage, FilesysCheckpointStorage):
                 path = os.path.join(storage.dirname(), fn)
                 os.makedirs(os.path.dirname(path), exist_ok=True)
-                xser_save(obj, path)
+                xser_save(obj, path, tensor_ids=ids, write_ref=ref)
             else:
                 storage.save_object(obj, fn)
             fault_point("ckpt_after_shard_write")
@@ -219,8 +267,19 @@ def save_checkpoint(checkpoint_dir_str: str, tag: str, model=None, optimizer=Non
         # one writer per distinct model shard: DP rank 0, or with EP the expert-data-parallel rank 0
         # of every EP rank (EDP replicas hold identical shards and would race on one path;
         # reference trainer/checkpoint.py:496)
-        if (get_expert_data_parallel_rank() == 0) if ep else (dpr == 0):
-            st.add_save_task(_model_state(model), os.path.join(str(tag), _get_path("model", ep=ep)), xser=use_xser)
+        group, gsize, grank = _model_replica_group()
+        fn = os.path.join(str(tag), _get_path("model", ep=ep))
+        if use_xser and gsize > 1:
+            # DP-deduplicated xser save (reference trainer/checkpoint.py:430-470): the replicas split
+            # the shard's tensor files by size; replica 0 also writes the structure and .info.pt
+            sd = _model_state(model)
+            _tag_expert_tensors(model, sd)
+            bins = assign_tensors_to_bins(xser_tensors(sd), gsize)
+            st.add_save_task(sd, fn, xser=True, xser_ids=bins[grank], xser_ref=(grank == 0))
+        elif (get_expert_data_parallel_rank() == 0) if ep else (dpr == 0):
+            sd = _model_state(model)
+            _tag_expert_tensors(model, sd)
+            st.add_save_task(sd, fn, xser=use_xser)
     if optimizer is not None:
         zero = zero1_optimizer or _is_zero1(optimizer)
         if zero or dpr == 0:
@@ -239,9 +298,28 @@ def finalize_checkpoint() -> None:
         g_iostate.finalize()
 
 
-def _load_obj(storage: BaseCheckpointStorage, filename: str, xser: bool, map_location):
+def _load_obj(storage: BaseCheckpointStorage, filename: str, xser: bool, map_location, replicas: bool = False):
     if xser and isinstance(storage, FilesysCheckpointStorage):
-        return xser_load(os.path.join(storage.dirname(), filename), map_location=map_location)
+        path = os.path.join(storage.dirname(), filename)
+        group, gsize, grank = _model_replica_group() if replicas else (None, 1, 0)
+        info = xser_load_info(path) if gsize > 1 else None
+        if info is None:
+            return xser_load(path, map_location=map_location)
+        # replicas read 1/N of the tensor files each and broadcast them to the others (reference
+        # _xser_load_data round-robin + broadcast, trainer/checkpoint.py:308-380)
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+            else torch.device("cpu")
+
+        def tensor_loader(tid, f):
+            owner = tid % gsize
+            if owner == grank:
+                t = torch.load(f, map_location=dev, weights_only=True).contiguous()
+            else:
+                t = torch.empty(tuple(info[tid]["shape"]), dtype=info[tid]["dtype"], device=dev)
+            dist.broadcast(t, src=dist.get_global_rank(group, owner), group=group)
+            return t   # stays on the broadcast device; load_state_dict copies into the parameters
+
+        return xser_load(path, map_location=map_location, tensor_loader=tensor_loader)
     return storage.load_object(filename, map_location=map_location, weights_only=True)
 
 
@@ -260,7 +338,7 @@ def load_checkpoint(path: str, tag: Optional[str] = None, model=None, optimizer=
     if model is not None:
         fn = os.path.join(tag, _get_path("model", ep=ep))
         xser = storage.dir_exists(fn + ".tensors")
-        sd = _load_obj(storage, fn, xser, "cpu")
+        sd = _load_obj(storage, fn, xser, "cpu", replicas=True)
         target = getattr(model, "module", model)
         if hasattr(model, "load_state_dict"):
             model.load_state_dict(sd, strict=strict)

@@ -412,3 +412,23 @@ def test_decode_attention_mfma_groups(D, Hq, Hkv, T, L):
     o2 = ops.decode_attention(q, kc, vc, seq, idx)
     ro2 = ops.decode_attention(q.cpu(), kc.cpu(), vc.cpu(), seq.cpu(), idx.cpu())
     assert _rel(o2.cpu(), ro2) < 2e-2
+
+
+def test_adamw_stochastic_rounding_matches_reference():
+    """bf16 copy-out with stochastic rounding: kernel bit-identical to the CPU emulation, unbiased."""
+    n = 1 << 20
+    p = (1.0 + torch.rand(n, device=DEV) * 2 ** -6)
+    g = torch.randn(n, device=DEV) * 1e-3
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    p16 = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    pc, gc, mc, vc = p.cpu().clone(), g.cpu(), m.cpu().clone(), v.cpu().clone()
+    p16c = torch.empty(n, dtype=torch.bfloat16)
+    ops.adamw_flat_(p, g, m, v, p16, 1e-3, 0.9, 0.95, 1e-8, 0.01, 1, sr_seed=987654321)
+    ops.adamw_flat_(pc, gc, mc, vc, p16c, 1e-3, 0.9, 0.95, 1e-8, 0.01, 1, sr_seed=987654321)
+    assert torch.allclose(p.cpu(), pc, rtol=0, atol=1e-6)
+    # identical fp32 masters -> identical stochastic bits
+    assert torch.equal(ops.stochastic_round_bf16(p.cpu(), 987654321), ops.stochastic_round_bf16(pc, 987654321))
+    assert torch.equal(p16.cpu(), ops.stochastic_round_bf16(p.cpu(), 987654321))
+    # unbiased: the mean rounding error is ~0 (round-to-nearest would be biased on this range)
+    err = (p16.float() - p).mean().item()
+    assert abs(err) < 2e-6, err

@@ -223,6 +223,12 @@ def _w_mixtral_ckpt(rank, world, ep, ckpt_dir, resume, out):
         losses.append(float(l) / world)
         if not resume and step == 2:
             nxd.save_checkpoint(ckpt_dir, "step_3", model=model, optimizer=opt, user_content={"step": 3})
+            sd = opt.state_dict()
+            # reference NeuronEPZero1Optimizer layout: dense entries, then expert entries at the offsets
+            for k in ("ep_param_id_offset", "ep_param_group_offset", "ep_base_state_offset", "ep_shape_info_offset"):
+                assert k in sd, k
+            assert len(sd["param_groups"]) == 2 * sd["ep_param_group_offset"]
+            assert all(b["name"].endswith(":ep") == (i >= sd["ep_base_state_offset"]) for i, b in sd["base_state"].items())
     nxd.finalize_checkpoint()
     if rank == 0:
         torch.save(losses, out)
