@@ -57,6 +57,8 @@ class InferenceConfig:
         self.temperature = kwargs.pop("temperature", 1.0)
         self.num_beams = kwargs.pop("num_beams", 1)
         self.use_hip_graphs = kwargs.pop("use_hip_graphs", True)
+        # GQA sharding (modules/gqa.py): "replicate-to-tp-degree" (default) | "convert-to-mha"
+        self.gqa_sharding_strategy = kwargs.pop("gqa_sharding_strategy", None)
         self.decode_graph_steps = kwargs.pop("decode_graph_steps", 16)
         self.torch_dtype = kwargs.pop("torch_dtype", "bfloat16")
         self.generation_config: Dict[str, Any] = kwargs.pop("generation_config", None) or {"max_length": seq_len}

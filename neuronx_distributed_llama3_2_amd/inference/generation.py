@@ -124,6 +124,21 @@ class LlamaForCausalLMInference:
             if not ps.model_parallel_is_initialized():
                 _init_single_process()
                 ps.initialize_model_parallel(tensor_model_parallel_size=1)
+        self._mha_from = None
+        strategy = getattr(config, "gqa_sharding_strategy", None)
+        nq = model_config.num_attention_heads
+        nkv = getattr(model_config, "num_key_value_heads", None) or nq
+        if strategy is not None and nkv < nq:
+            from ..modules.gqa import GQA, determine_sharding_strategy
+
+            if determine_sharding_strategy(config.tp_degree, nkv, strategy) == GQA.CONVERT_TO_MHA:
+                # reference examples/inference/modules/gqa.py: K/V heads replicated to one per Q head
+                import copy as _copy
+
+                self._mha_from = (nq, nkv, getattr(model_config, "head_dim", None) or model_config.hidden_size // nq)
+                model_config = _copy.copy(model_config)
+                model_config.num_key_value_heads = nq
+                self.model_config = model_config
         self.model = self._model_cls(model_config, dtype=dtype,
                                      device=torch.device("meta") if not init_weights else self.device)
         if config.quantized:
@@ -167,6 +182,10 @@ class LlamaForCausalLMInference:
         return self
 
     def _load_full(self, full_sd: Dict[str, torch.Tensor]) -> None:
+        if self._mha_from is not None:
+            from ..modules.gqa import convert_state_dict_to_mha
+
+            full_sd = convert_state_dict_to_mha(full_sd, *self._mha_from)
         tp, rank = ps.get_tensor_model_parallel_size(), ps.get_tensor_model_parallel_rank()
         local = shard_state_dict(self.model, full_sd, tp, rank, strict=False)
         self._load_local(local)

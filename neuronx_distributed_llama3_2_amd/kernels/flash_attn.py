@@ -16,13 +16,32 @@ from typing import Optional
 
 import torch
 
+from ..ops.attention_dropout import attention_with_dropout
 from ..ops.flash_attn import flash_attn_func as _fa
 
 
+def _dropout_attn(q, k, v, causal, softmax_scale, layout, dropout_p, seed):
+    """dropout_p > 0: the chunked flash decomposition with a hashed keep mask (ops/attention_dropout.py);
+    heads are numbered globally across tensor-parallel ranks so the mask matches the unsharded model."""
+    from ..parallel_layers import parallel_state as ps
+
+    if layout == "bshd":
+        q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+    elif layout == "nki":
+        q, k, v = q.transpose(2, 3), k.transpose(2, 3), v
+    elif layout != "bhsd":
+        raise ValueError(f"unknown layout {layout}")
+    off = ps.get_tensor_model_parallel_rank() * q.shape[1] if ps.model_parallel_is_initialized() else 0
+    o = attention_with_dropout(q, k, v, dropout_p, causal=causal, softmax_scale=softmax_scale, seed=seed,
+                               head_offset=off)
+    return o.transpose(1, 2) if layout == "bshd" else o
+
+
 def flash_attn_func(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True,
-                    softmax_scale: Optional[float] = None, layout: str = "bhsd", dropout_p: float = 0.0) -> torch.Tensor:
+                    softmax_scale: Optional[float] = None, layout: str = "bhsd", dropout_p: float = 0.0,
+                    seed: Optional[int] = None) -> torch.Tensor:
     if dropout_p:
-        raise NotImplementedError("attention dropout is not supported (Llama-3 trains without it)")
+        return _dropout_attn(q, k, v, causal, softmax_scale, layout, dropout_p, seed)
     if layout == "bshd":
         return _fa(q, k, v, causal=causal, softmax_scale=softmax_scale)
     if layout == "bhsd":
@@ -36,7 +55,7 @@ def flash_attn_func(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: b
 
 
 def nki_flash_attn_func(query, key, value, droupout_p: float = 0.0, softmax_scale: Optional[float] = None,
-                        causal: bool = True):
+                        causal: bool = True, seed: Optional[int] = None):
     """Reference-named alias: query/key [B, H, D, S], value [B, H, S, D] -> [B, H, S, D]."""
     return flash_attn_func(query, key, value, causal=causal, softmax_scale=softmax_scale, layout="nki",
-                           dropout_p=droupout_p)
+                           dropout_p=droupout_p, seed=seed)

@@ -17,6 +17,8 @@ import enum
 import math
 from typing import Optional, Tuple, Union
 
+import torch
+
 
 class GQA(enum.Enum):
     CONVERT_TO_MHA = "convert-to-mha"
@@ -63,3 +65,30 @@ def kv_size_multiplier(tp_degree: int, num_attention_heads: int, num_key_value_h
     strategy = determine_sharding_strategy(tp_degree, num_key_value_heads, sharding_strategy)
     _, kv = get_shardable_head_counts(tp_degree, num_attention_heads, num_key_value_heads, strategy)
     return max(minimum, kv // num_key_value_heads)
+
+
+def replicate_kv(tensor, source_heads: int, repeats: int, head_dim: int = 0):
+    """Repeat every K/V head `repeats` times in place along `head_dim` (heads are contiguous blocks
+    of that dim): [K0, K1] -> [K0, K0, K1, K1] for repeats 2."""
+    if tensor is None or repeats == 1:
+        return tensor
+    shape = tensor.shape[:head_dim] + (source_heads, tensor.shape[head_dim] // source_heads) + tensor.shape[head_dim + 1:]
+    t = tensor.reshape(shape).repeat_interleave(repeats, dim=head_dim)
+    return t.reshape(tensor.shape[:head_dim] + (-1,) + tensor.shape[head_dim + 1:])
+
+
+def convert_state_dict_to_mha(full_sd, num_attention_heads: int, num_key_value_heads: int, head_dim: int):
+    """CONVERT_TO_MHA on a full (unsharded) framework state dict: the K/V rows of every fused
+    `qkv_proj.{weight,bias}_qkv` are replicated so query head i gets its own copy of its K/V head
+    (i // group); the model is then built with num_key_value_heads = num_attention_heads."""
+    g = num_attention_heads // num_key_value_heads
+    if g == 1:
+        return dict(full_sd)
+    out = {}
+    qd, kd = num_attention_heads * head_dim, num_key_value_heads * head_dim
+    for k, v in full_sd.items():
+        if k.endswith("qkv_proj.weight_qkv") or k.endswith("qkv_proj.bias_qkv"):
+            q, kk, vv = v.split([qd, kd, kd], dim=0)
+            v = torch.cat([q, replicate_kv(kk, num_key_value_heads, g), replicate_kv(vv, num_key_value_heads, g)], 0)
+        out[k] = v
+    return out

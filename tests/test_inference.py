@@ -264,3 +264,35 @@ def test_tree_attention_chain_equals_decode():
     m.kv_cache[:, :, 0, :, 10:14] = 0
     m.commit_tree_kv(kvs, torch.arange(4), 10)
     assert torch.allclose(m.kv_cache[:, :, 0, :, 10:14], kc, atol=1e-5)
+
+
+def _w_mha(rank, world, out_path):
+    cfg = _tiny_cfg(num_attention_heads=4, num_key_value_heads=1)
+    hf = _hf_model(cfg)
+    sd = {k: v.detach() for k, v in hf.state_dict().items()}
+    m = _inf_model(cfg, sd, tp=world, gqa_sharding_strategy="convert-to-mha")
+    assert m.model_config.num_key_value_heads == 4 and m.model.nkv == 4 // world
+    ids = torch.randint(3, cfg.vocab_size, (2, 12), generator=torch.Generator().manual_seed(0))
+    out = m.generate(ids, max_new_tokens=6, eos_token_id=-1)
+    if rank == 0:
+        with torch.no_grad():
+            ref = hf(ids).logits[:, -1]
+        torch.save({"out": out, "ref_next": ref.argmax(-1)}, out_path)
+
+
+def test_gqa_convert_to_mha_matches_hf_and_tp1():
+    """GQA.CONVERT_TO_MHA (reference examples/inference/modules/gqa.py): one K/V copy per query
+    head, same tokens as the HF model's greedy choice and as TP=1."""
+    from neuronx_distributed_llama3_2_amd.modules.gqa import GQA, determine_sharding_strategy, get_shardable_head_counts
+
+    assert determine_sharding_strategy(32, 8) == GQA.REPLICATE_TO_TP_DEGREE
+    assert determine_sharding_strategy(12, 8) == GQA.CONVERT_TO_MHA
+    assert get_shardable_head_counts(32, 32, 8, GQA.CONVERT_TO_MHA) == (32, 32)
+    assert get_shardable_head_counts(32, 32, 8, GQA.REPLICATE_TO_TP_DEGREE) == (32, 32)
+    assert get_shardable_head_counts(4, 32, 8, GQA.REPLICATE_TO_TP_DEGREE) == (32, 8)
+    d = tempfile.mkdtemp()
+    run_distributed(_w_mha, 1, os.path.join(d, "a.pt"))
+    run_distributed(_w_mha, 2, os.path.join(d, "b.pt"))
+    a, b = torch.load(os.path.join(d, "a.pt")), torch.load(os.path.join(d, "b.pt"))
+    assert torch.equal(a["out"], b["out"])
+    assert torch.equal(a["out"][:, 12], a["ref_next"])
