@@ -10,12 +10,14 @@ against its public API and import-gated (parity unpinned by tests here).
 """
 
 from ._compat import HAVE_LIGHTNING, require_lightning  # noqa: F401
+from .launcher import NeuronLauncher  # noqa: F401  (no Lightning dependency)
 
 _EXPORTS = {
     "NeuronXLAStrategy": ".strategy", "NxDStrategy": ".strategy",
     "NeuronXLAAccelerator": ".accelerator", "NeuronCheckpointIO": ".checkpoint_io",
     "NeuronLTModule": ".module", "NeuronXLAPrecisionPlugin": ".precision_plugin",
     "NeuronTQDMProgressBar": ".progress_bar", "NeuronTensorBoardLogger": ".logger",
+    "_NeuronXLALauncher": ".launcher",
 }
 
 

@@ -32,6 +32,11 @@ class NeuronXLAStrategy(DDPStrategy):
         self.expert_parallel_size = expert_parallel_size
         self.debug = debug
 
+    def _configure_launcher(self) -> None:
+        from .launcher import _NeuronXLALauncher
+
+        self._launcher = _NeuronXLALauncher(self)
+
     def setup_distributed(self) -> None:
         super().setup_distributed()
         if not ps.model_parallel_is_initialized():
