@@ -4,12 +4,20 @@ from one process; trace/model_builder.py:130-261 spawns rank processes).
 
 Each worker initialises torch.distributed (RCCL over xGMI when there is a GPU per rank, gloo on
 the CPU otherwise), builds and captures its shard through a picklable `build_fn(rank, world,
-*args)`, then serves commands from its queue.  A forward sends the (host) inputs to every rank;
-every rank replays its graphs (their collectives meet over RCCL); rank 0 returns the outputs.
+*args)`, then serves commands from its queue.  A forward makes every rank replay its graphs
+(their collectives meet over RCCL); rank 0 returns the outputs.
+
+Tensor I/O goes through PERSISTENT shared-memory buffers, not through the command queues: the
+controller copies each input into its bound shared input buffer (re-bound only when a larger
+shape arrives), every rank views the same pages and copies them to its GPU; rank 0 writes the
+outputs into shared output buffers it handed to the controller once.  A call's queue traffic is
+a few small tuples (shapes / dtypes), so the per-call cost is two memcpys plus the H2D / D2H
+copies, independent of how the tensors were produced.
 """
 
 from __future__ import annotations
 
+import math
 import os
 import socket
 import traceback
@@ -35,6 +43,53 @@ def _to_host(x):
     if isinstance(x, dict):
         return {k: _to_host(v) for k, v in x.items()}
     return x
+
+
+class _SharedSlots:
+    """Growable set of shared-memory CPU buffers, one per tensor position of a call."""
+
+    def __init__(self):
+        self.bufs: List[torch.Tensor] = []
+
+    def fit(self, tensors: List[torch.Tensor]) -> bool:
+        """Make every slot large enough and of the right dtype; True when (re)allocation happened
+        (the new buffers must then be handed to the other side)."""
+        changed = len(self.bufs) != len(tensors)
+        new = []
+        for i, t in enumerate(tensors):
+            b = self.bufs[i] if i < len(self.bufs) else None
+            if b is None or b.dtype != t.dtype or b.numel() < t.numel():
+                b = torch.empty(max(t.numel(), 1), dtype=t.dtype).share_memory_()
+                changed = True
+            new.append(b)
+        self.bufs = new
+        return changed
+
+    def write(self, tensors: List[torch.Tensor]):
+        meta = []
+        for b, t in zip(self.bufs, tensors):
+            b[:t.numel()].copy_(t.detach().reshape(-1), non_blocking=False)
+            meta.append(tuple(t.shape))
+        return meta
+
+    def views(self, meta):
+        return [b[:math.prod(shape)].view(shape) for b, shape in zip(self.bufs, meta)]
+
+
+def _flatten_out(out):
+    """(tensors, structure) of a forward's output: a tensor or a (nested) list / tuple of them."""
+    if isinstance(out, torch.Tensor):
+        return [out], "T"
+    if isinstance(out, (list, tuple)) and all(isinstance(o, torch.Tensor) for o in out):
+        return list(out), ("L" if isinstance(out, list) else "U", len(out))
+    return None, None
+
+
+def _unflatten_out(tensors, structure):
+    if structure == "T":
+        return tensors[0]
+    kind, _ = structure
+    return list(tensors) if kind == "L" else tuple(tensors)
 
 
 def _to_dev(x, dev):
@@ -71,12 +126,31 @@ def _worker_main(rank, world, port, build_fn, build_args, cmd_q, res_q):
     except Exception:
         res_q.put(("err", rank, traceback.format_exc()))
         return
+    in_slots = _SharedSlots()
+    out_slots = _SharedSlots()
     while True:
         cmd, payload = cmd_q.get()
         if cmd == "stop":
             break
         try:
-            if cmd == "forward":
+            if cmd == "bind":         # new shared input buffers (shape growth / first call)
+                in_slots.bufs = list(payload)
+                res_q.put(("ok", rank, None))
+            elif cmd == "forward_shm":
+                inputs = [v.to(dev, non_blocking=False) for v in in_slots.views(payload)]
+                out = obj(*inputs)
+                reply = None
+                if rank == 0:
+                    tensors, structure = _flatten_out(out)
+                    if tensors is None:                       # not tensor-shaped: plain (pickled) reply
+                        reply = ("obj", _to_host(out))
+                    else:
+                        host = [t.detach().cpu() for t in tensors]
+                        rebound = out_slots.fit(host)
+                        meta = out_slots.write(host)
+                        reply = ("shm", structure, meta, out_slots.bufs if rebound else None)
+                res_q.put(("ok", rank, reply))
+            elif cmd == "forward":
                 out = obj(*_to_dev(payload, dev))
                 res_q.put(("ok", rank, _to_host(out) if rank == 0 else None))
             elif cmd == "call":      # (method name, args): e.g. save
@@ -103,6 +177,8 @@ class SpmdWorkerPool:
                       for r in range(world)]
         for p in self.procs:
             p.start()
+        self._in_slots = _SharedSlots()
+        self._out_slots = _SharedSlots()
         self._collect()
 
     def _collect(self):
@@ -119,10 +195,28 @@ class SpmdWorkerPool:
         return results[0]
 
     def forward(self, *inputs: torch.Tensor):
-        host = _to_host(list(inputs))
+        if not all(isinstance(t, torch.Tensor) for t in inputs):
+            host = _to_host(list(inputs))
+            for q in self.cmd_q:
+                q.put(("forward", host))
+            return self._collect()
+        slots = self._in_slots
+        if slots.fit(list(inputs)):
+            for q in self.cmd_q:
+                q.put(("bind", slots.bufs))
+            self._collect()
+        meta = slots.write(list(inputs))
         for q in self.cmd_q:
-            q.put(("forward", host))
-        return self._collect()
+            q.put(("forward_shm", meta))
+        reply = self._collect()
+        if reply[0] == "obj":
+            return reply[1]
+        _, structure, out_meta, new_bufs = reply
+        if new_bufs is not None:
+            self._out_slots.bufs = list(new_bufs)
+        # copy out of the shared buffers: the next call overwrites them
+        outs = [v.clone() for v in self._out_slots.views(out_meta)]
+        return _unflatten_out(outs, structure)
 
     __call__ = forward
 

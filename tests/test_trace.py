@@ -147,3 +147,30 @@ def test_lightning_gated_import():
         return
     with pytest.raises(ImportError, match="Lightning"):
         L.NeuronXLAStrategy
+
+
+def _pool_sum_build(rank, world):
+    import torch.distributed as dist
+
+    def fn(x, y):
+        t = x.float().clone() * (rank + 1)
+        dist.all_reduce(t)
+        return t, y + 1
+    return fn
+
+
+def test_spmd_pool_shared_memory_io_with_shape_growth():
+    """Tensor I/O through persistent shared buffers: growth re-binds, smaller calls reuse them."""
+    from neuronx_distributed_llama3_2_amd.trace.runtime import SpmdWorkerPool
+
+    pool = SpmdWorkerPool(2, _pool_sum_build)
+    try:
+        for shape in [(2, 3), (5, 7), (2, 3), (1,)]:
+            x = torch.randn(*shape)
+            y = torch.arange(4, dtype=torch.int64)
+            a, b = pool(x, y)
+            torch.testing.assert_close(a, x * 3)
+            assert torch.equal(b, y + 1) and a.shape == x.shape
+        assert pool._in_slots.bufs[0].numel() == 35   # grew once, then reused
+    finally:
+        pool.close()
