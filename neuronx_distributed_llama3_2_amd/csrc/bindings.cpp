@@ -30,7 +30,7 @@ int xent_bwd_launch(const void*, int, const int64_t*, const float*, void*, int64
                     int64_t, hipStream_t);
 int flat_reduce_launch(const void*, int, int64_t, int, float*, float*, int, hipStream_t);
 int adamw_flat_launch(float*, const void*, int, float*, float*, void*, int64_t, float, float, float, float, float, float,
-                      float, const float*, float, uint32_t, hipStream_t);
+                      float, const float*, float, uint32_t, const float*, hipStream_t);
 int clip_coef_launch(const float*, float*, float, int, hipStream_t);
 int scale_flat_launch(float*, int64_t, const float*, hipStream_t);
 int embedding_fwd_launch(const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, hipStream_t);
@@ -303,7 +303,7 @@ void flat_reduce(at::Tensor x, int64_t mode, at::Tensor out, bool accumulate) {
 
 void adamw_flat(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, c10::optional<at::Tensor> p16, double lr, double b1,
                 double b2, double eps, double wd, double bc1, double bc2, c10::optional<at::Tensor> gscale, double gscale_host,
-                int64_t sr_seed) {
+                int64_t sr_seed, c10::optional<at::Tensor> hyper) {
   flat_check(p, "p");
   flat_check(g, "g");
   flat_check(m, "m");
@@ -324,9 +324,14 @@ void adamw_flat(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, c10::opt
     TORCH_CHECK(gscale->scalar_type() == at::kFloat && gscale->is_cuda(), "gscale must be a fp32 GPU tensor");
     gs = gscale->data_ptr<float>();
   }
+  if (hyper.has_value()) {
+    TORCH_CHECK(hyper->scalar_type() == at::kFloat && hyper->is_cuda() && hyper->numel() >= 3 && hyper->is_contiguous(),
+                "hyper must be a contiguous fp32 GPU tensor [lr, bc1, bc2]");
+  }
   check_rc(nxd::adamw_flat_launch(p.data_ptr<float>(), g.data_ptr(), g.scalar_type() == at::kBFloat16, m.data_ptr<float>(),
                                   v.data_ptr<float>(), o, n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1,
-                                  (float)bc2, gs, (float)gscale_host, (uint32_t)(sr_seed & 0xffffffff), cur_stream()),
+                                  (float)bc2, gs, (float)gscale_host, (uint32_t)(sr_seed & 0xffffffff),
+                                  hyper.has_value() ? hyper->data_ptr<float>() : nullptr, cur_stream()),
            "adamw_flat");
 }
 

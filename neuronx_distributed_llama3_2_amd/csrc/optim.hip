@@ -90,10 +90,18 @@ __device__ __forceinline__ uint16_t f2bf_sr(float f, uint32_t seed, int64_t idx)
   return (uint16_t)((u + r) >> 16);
 }
 
+// hyper (nullable): device [lr, 1 - beta1^t, 1 - beta2^t] overriding h.lr / h.bc1 / h.bc2, so a
+// captured optimizer step (hipGraph) replays with the current step's values.
 template <bool GBF16, bool HAS_OUT>
 __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const void* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, uint16_t* __restrict__ p16, int64_t n, AdamHyper h,
-                                                    const float* __restrict__ gscale_ptr, float gscale_host) {
+                                                    const float* __restrict__ gscale_ptr, float gscale_host,
+                                                    const float* __restrict__ hyper) {
+  if (hyper) {
+    h.lr = hyper[0];
+    h.bc1 = hyper[1];
+    h.bc2 = hyper[2];
+  }
   const float gs = gscale_ptr ? gscale_ptr[0] * gscale_host : gscale_host;
   const float step = h.lr / h.bc1;
   const float rbc2 = rsqrtf(h.bc2);
@@ -174,12 +182,12 @@ int flat_reduce_launch(const void* x, int is_bf16, int64_t n, int mode, float* p
 
 int adamw_flat_launch(float* p, const void* g, int g_is_bf16, float* m, float* v, void* p16, int64_t n, float lr, float beta1,
                       float beta2, float eps, float wd, float bc1, float bc2, const float* gscale_ptr, float gscale_host,
-                      uint32_t sr_seed, hipStream_t stream) {
+                      uint32_t sr_seed, const float* hyper, hipStream_t stream) {
   using namespace optim;
   if (n == 0) return 0;
   AdamHyper h{lr, beta1, beta2, eps, wd, bc1, bc2, sr_seed};
   const int grid = grid_for(n / 4);
-#define AK(B, O) hipLaunchKernelGGL((adamw_kernel<B, O>), dim3(grid), dim3(256), 0, stream, p, g, m, v, (uint16_t*)p16, n, h, gscale_ptr, gscale_host)
+#define AK(B, O) hipLaunchKernelGGL((adamw_kernel<B, O>), dim3(grid), dim3(256), 0, stream, p, g, m, v, (uint16_t*)p16, n, h, gscale_ptr, gscale_host, hyper)
   if (g_is_bf16) { if (p16) AK(true, true); else AK(true, false); }
   else { if (p16) AK(false, true); else AK(false, false); }
 #undef AK

@@ -101,9 +101,10 @@ def sr_seed_for_step(step: int, base: int = 0x5EED) -> int:
 def adamw_flat_(p32: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
                 p16: Optional[torch.Tensor], lr: float, beta1: float, beta2: float, eps: float, weight_decay: float,
                 step: int, grad_scale: Optional[torch.Tensor] = None, grad_scale_host: float = 1.0,
-                bias_correction: bool = True, sr_seed: int = 0) -> None:
+                bias_correction: bool = True, sr_seed: int = 0, hyper: Optional[torch.Tensor] = None) -> None:
     """In-place AdamW (decoupled weight decay) over flat fp32 buffers; writes bf16 params to p16
-    (stochastically rounded when sr_seed != 0)."""
+    (stochastically rounded when sr_seed != 0).  hyper: optional device [lr, 1-beta1^t, 1-beta2^t]
+    read by the kernel instead of lr / step (graph-captured optimizer steps)."""
     from .gemm import weights_updated
 
     weights_updated()   # the kernel writes weights behind autograd: K-major dgrad copies go stale
@@ -111,8 +112,10 @@ def adamw_flat_(p32: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, ex
     bc2 = 1.0 - beta2 ** step if bias_correction else 1.0
     if use_native(p32, grad):
         ext().adamw_flat(p32, grad, exp_avg, exp_avg_sq, p16, lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale,
-                         grad_scale_host, int(sr_seed))
+                         grad_scale_host, int(sr_seed), hyper)
         return
+    if hyper is not None:
+        lr, bc1, bc2 = (float(x) for x in hyper[:3].tolist())
     g = grad.float() * grad_scale_host
     if grad_scale is not None:
         g = g * grad_scale[0]

@@ -95,6 +95,36 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
                 st.param_index = [index_of[id(p)] for p in plist]   # registration order
                 self.buffers.append(st)
 
+    # ---------------------------------------------------------------- graph capture
+    @property
+    def capturable(self) -> bool:
+        return getattr(self, "_capturable", False)
+
+    def make_capturable(self) -> None:
+        """Move the per-step scalars to the device so step() can be captured in a hipGraph: the
+        step counter lives in a device tensor, bias corrections are computed on the device each
+        step, and the kernels read [lr, 1-beta1^t, 1-beta2^t] from memory.  Learning rates set in
+        param_groups reach the device through sync_lr() (called by GraphedTrainStep per replay)."""
+        dev = self.buffers[0].master.device
+        self._capturable = True
+        self._dev_step = torch.full((1,), float(self.step_count), dtype=torch.float32, device=dev)
+        self._dev_hyper = torch.zeros(len(self.param_groups), 3, dtype=torch.float32, device=dev)
+        self._dev_betas = torch.tensor([list(g["betas"]) for g in self.param_groups], dtype=torch.float32, device=dev)
+        self.sync_lr()
+
+    def sync_lr(self) -> None:
+        if self.capturable:
+            lrs = torch.tensor([float(g["lr"]) for g in self.param_groups], dtype=torch.float32)
+            self._dev_hyper[:, 0].copy_(lrs, non_blocking=True)
+
+    def _device_hyper_step(self) -> torch.Tensor:
+        self._dev_step.add_(1.0)
+        if self.bias_correction:
+            self._dev_hyper[:, 1:].copy_(1.0 - torch.pow(self._dev_betas, self._dev_step))
+        else:
+            self._dev_hyper[:, 1:].fill_(1.0)
+        return self._dev_hyper
+
     # ---------------------------------------------------------------- helpers
     def set_grad_sync(self, enabled: bool) -> None:
         for b in self.buffers:
@@ -152,6 +182,7 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
             self.grad_norm = coef[1]
         self.step_count += 1
         seed = ops.sr_seed_for_step(self.step_count) if self.stochastic_rounding else 0
+        hyper = self._device_hyper_step() if self.capturable else None
         for bi, b in enumerate(self.buffers):
             g = b.group
             beta1, beta2 = g["betas"]
@@ -160,7 +191,8 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
                 ops.adamw_flat_(b.master[lo:lo + n], b.buf.grad_data[s:e], b.exp_avg[lo:lo + n], b.exp_avg_sq[lo:lo + n],
                                 b.buf.param_data[s:e], g["lr"], beta1, beta2, g["eps"], g["weight_decay"], self.step_count,
                                 grad_scale=coef, bias_correction=self.bias_correction,
-                                sr_seed=(((seed ^ (bi * 0x9E3779B1 + s)) & 0xFFFFFFFF) or 1) if seed else 0)
+                                sr_seed=(((seed ^ (bi * 0x9E3779B1 + s)) & 0xFFFFFFFF) or 1) if seed else 0,
+                                hyper=hyper[b.group_index] if hyper is not None else None)
         for b in self.buffers:
             b.buf.gather_params()
         return loss
@@ -183,9 +215,12 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
             return self._load_full_state_dict(sd)
         assert sd.get("flat_optimizer"), "not a FlatMixedPrecisionAdamW state dict"
         self.step_count = int(sd["step"])
+        if self.capturable:
+            self._dev_step.fill_(float(self.step_count))
         for g, sg in zip(self.param_groups, sd["param_groups"]):
             for k, v in sg.items():
                 g[k] = v
+        self.sync_lr()
         for b, sb in zip(self.buffers, sd["buffers"]):
             assert b.buf.name == sb["name"] and b.master.numel() == sb["master"].numel(), "optimizer layout mismatch"
             b.master.copy_(sb["master"])
