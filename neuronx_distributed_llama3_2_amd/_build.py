@@ -37,7 +37,9 @@ def _torch_flags():
     import torch
 
     tdir = Path(torch.__file__).resolve().parent
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
     inc = [
+        f"-I{os.path.join(rocm, 'include')}",
         f"-I{tdir / 'include'}",
         f"-I{tdir / 'include' / 'torch' / 'csrc' / 'api' / 'include'}",
         f"-I{sysconfig.get_paths()['include']}",
@@ -52,7 +54,7 @@ def _torch_flags():
     ]
     libdir = tdir / "lib"
     libs = [f"-L{libdir}", f"-Wl,-rpath,{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip",
-            "-ltorch_hip", "-lamdhip64", "-lhipblaslt"]
+            "-ltorch_hip", "-lamdhip64", "-lhipblaslt", "-ldl"]
     return inc, defs, libs
 
 

@@ -687,10 +687,12 @@ void dgemv(int64_t epi, at::Tensor x, c10::optional<at::Tensor> norm_w, double e
 
 void register_gemm(pybind11::module& m);  // gemm.cpp
 void register_dataloader(pybind11::module& m);  // dataloader.cpp
+void register_comm(pybind11::module& m);  // comm.cpp
 
 PYBIND11_MODULE(_C, m) {
   register_gemm(m);
   register_dataloader(m);
+  register_comm(m);
   m.def("gemv", &gemv);
   m.def("dequant_int8", &dequant_int8);
   m.def("expert_gemv", &expert_gemv);
