@@ -46,6 +46,7 @@ struct FwdParams {
   int causal;
   int causal_offset;  // query i attends keys <= i + causal_offset (Sk - Sq for bottom-right alignment)
   int prio_hi;        // static s_setprio 1 for the second half of an 8-wave workgroup (MI355X_MICROARCH item 4)
+  int xcd_map;        // block -> (head, q block) map: 0 contiguous per XCD, 1 balanced kv-head-per-XCD, 2 interleaved
 };
 
 // 16-byte chunk swizzle of a [rows][D] bf16 LDS image (D/8 chunks per row).
@@ -114,11 +115,37 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
 
   const int nblk_m = (p.Sq + kBlockM - 1) / kBlockM;
   const int nwg = gridDim.x;
-  const int L = xcd_remap(blockIdx.x, nwg);
-  const int bh = L % (p.B * p.Hq);
-  const int mblk = nblk_m - 1 - L / (p.B * p.Hq);  // heavy (late) causal blocks first
-  const int b = bh / p.Hq, hq = bh % p.Hq;
-  const int hkv = hq / (p.Hq / p.Hkv);
+  int b, hq, hkv, mblk;
+  if (p.xcd_map == 1) {
+    // Balanced XCD map (workgroup id x lands on XCD x % 8, in dispatch order x / 8): XCD x owns the
+    // kv heads {x, x + 8, ...} of every batch -- each XCD gets the SAME mix of causal block sizes
+    // (equal work per XCD) and every q head of a GQA group next to its K/V in one L2 -- walked
+    // heavy blocks first.  Needs B * Hkv % 8 == 0 (host-checked).
+    const int G = p.Hq / p.Hkv;
+    const int xcd = blockIdx.x & 7, i = blockIdx.x >> 3;
+    const int per_m = (p.B * p.Hkv / 8) * G;
+    mblk = nblk_m - 1 - i / per_m;
+    const int j = i % per_m;
+    const int bkv = (j / G) * 8 + xcd;
+    b = bkv / p.Hkv;
+    hkv = bkv % p.Hkv;
+    hq = hkv * G + j % G;
+  } else if (p.xcd_map == 2) {
+    // interleaved: dispatch order IS the heavy-first order, consecutive items on different XCDs
+    const int bh = blockIdx.x % (p.B * p.Hq);
+    mblk = nblk_m - 1 - blockIdx.x / (p.B * p.Hq);
+    b = bh / p.Hq;
+    hq = bh % p.Hq;
+    hkv = hq / (p.Hq / p.Hkv);
+  } else {
+    // contiguous ranges per XCD (round 1): XCD 0 receives the heaviest causal rows
+    const int L = xcd_remap(blockIdx.x, nwg);
+    const int bh = L % (p.B * p.Hq);
+    mblk = nblk_m - 1 - L / (p.B * p.Hq);  // heavy (late) causal blocks first
+    b = bh / p.Hq;
+    hq = bh % p.Hq;
+    hkv = hq / (p.Hq / p.Hkv);
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -455,6 +482,9 @@ int flash_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, 
   const bool ring3 = (var & 16) && pipe;
   const bool kt128 = (var & 32) && pipe;
   p.prio_hi = (var & 8) ? 1 : 0;
+  // causal block-to-XCD map (variant bits 64/128): 64 = balanced kv-head-per-XCD when B * Hkv % 8 == 0
+  // (else interleaved), 128 = always interleaved, neither = contiguous ranges per XCD (round 1)
+  p.xcd_map = (var & 128) ? 2 : ((var & 64) ? (((B * Hkv) % 8 == 0) ? 1 : 2) : 0);
   bool w8 = var & 1;
   if (w8 && ((Sq + 255) / 256) * B * Hq < 512) w8 = false;
   const int rows = w8 ? 256 : 128;
