@@ -62,6 +62,7 @@ struct BwdParams {
   int causal;
   int causal_offset;
   int chunk;   // max (q head, q tile) iterations per work item
+  int xcd_map; // 0: contiguous item ranges per XCD, 2: interleaved (see bwd_kernel)
   int ablate;  // timing-only ablations (NXD_FAB_ABLATE; outputs wrong): 1 no dQ atomics,
                // 2 no dK/dV atomics, 4 no dQ MFMAs, 8 no dV/dK MFMAs, 16 no Q/dO tile loads,
                // 32 no per-tile barriers
@@ -156,7 +157,10 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
 
   const int G = p.Hq / p.Hkv;
   const int BH = p.B * p.Hkv;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  // work-item order = dispatch order (xcd_map 2: consecutive items on different XCDs, so every XCD
+  // gets the same mix of heavy and light items) or contiguous item ranges per XCD (0, round 1: the
+  // first XCD received all of the heaviest key blocks' items)
+  const int L = p.xcd_map == 2 ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   const int bh = L % BH;
   int kc = L / BH;
   // ---- decode (key block, chunk) of this work item: key blocks in order (heaviest first)
@@ -649,7 +653,14 @@ int choose_chunk(int nkb, int Sq, int G, int causal, int off, int BH, int ncu) {
 
 // tuning knobs, resolved once at load (NXD_FAB_ABLATE / NXD_FAB_CHUNK) and settable from Python
 // (flash_attn_set_knob) for in-process A/B — no per-launch getenv
-static int g_ablate = -1, g_chunk = -1;
+static int g_ablate = -1, g_chunk = -1, g_xcd = -1;
+int xcd_map_mode() {
+  if (g_xcd < 0) {
+    const char* e = getenv("NXD_FAB_XCD_MAP");
+    g_xcd = e ? atoi(e) : 2;
+  }
+  return g_xcd;
+}
 int ablate_flags() {
   if (g_ablate < 0) {
     const char* e = getenv("NXD_FAB_ABLATE");
@@ -670,6 +681,7 @@ int chunk_override() {
 void flash_attn_bwd_set_knob(int which, int value) {
   if (which == 0) fab::g_ablate = value;
   if (which == 1) fab::g_chunk = value;
+  if (which == 3) fab::g_xcd = value;
 }
 
 // fp32 workspace floats the backward needs: dq_acc + dk_acc + dv_acc + nlse + ndelta
@@ -727,6 +739,7 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   for (int kb = 0; kb < nkb; ++kb) items += (kb_iters(kb, Sq, G, causal, causal_offset) + p.chunk - 1) / p.chunk;
   items *= (int64_t)B * Hkv;
   p.ablate = ablate_flags();
+  p.xcd_map = xcd_map_mode();
   if (items > 0) {
     if (D == 128) {
       const size_t lds = kBlockK * 128 * 2 + 4 * kBlockQ * 128 * 2 + kBlockK * 64 + 512 + 128 * 128 * 2;

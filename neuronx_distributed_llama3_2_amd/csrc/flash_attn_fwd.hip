@@ -442,7 +442,7 @@ static int g_fwd_variant = -1;
 static int fwd_variant() {
   if (g_fwd_variant < 0) {
     const char* e = getenv("NXD_FA_FWD_VARIANT");
-    g_fwd_variant = e ? atoi(e) : 13;
+    g_fwd_variant = e ? atoi(e) : 141;   // 13 | 128: interleaved block->XCD map (profiles/r2_fa_xcd_map_ab.jsonl)
   }
   return g_fwd_variant;
 }
