@@ -10,7 +10,8 @@ import csv
 import sys
 from collections import defaultdict
 
-KEYS = ("fa::fwd_kernel", "fab::bwd_kernel", "fab::", "rms::", "rmsnorm", "swiglu", "xent", "adamw", "rope", "embedding")
+KEYS = ("fa::fwd_kernel", "fab::bwd_kernel", "fab::", "rms::", "rmsnorm", "swiglu", "xent", "adamw", "rope", "embedding",
+        "gg::grouped_gemm", "dfused::", "dattn::")
 
 
 def short(name):
