@@ -59,6 +59,8 @@ class InferenceConfig:
         self.use_hip_graphs = kwargs.pop("use_hip_graphs", True)
         # GQA sharding (modules/gqa.py): "replicate-to-tp-degree" (default) | "convert-to-mha"
         self.gqa_sharding_strategy = kwargs.pop("gqa_sharding_strategy", None)
+        # measured weight-layout pass at the context-encoding size (trace/weight_layout.py)
+        self.weight_layout_optimization = kwargs.pop("weight_layout_optimization", False)
         self.decode_graph_steps = kwargs.pop("decode_graph_steps", 16)
         self.torch_dtype = kwargs.pop("torch_dtype", "bfloat16")
         self.generation_config: Dict[str, Any] = kwargs.pop("generation_config", None) or {"max_length": seq_len}

@@ -210,6 +210,11 @@ class LlamaForCausalLMInference:
             p.requires_grad_(False)
         if hasattr(self.model, "post_load"):
             self.model.post_load()
+        if getattr(self.config, "weight_layout_optimization", False):
+            from ..trace.weight_layout import optimize_weight_layout
+
+            self.weight_layouts = optimize_weight_layout(self.model, int(self.config.max_context_length) * self.max_batch,
+                                                         path=getattr(self, "_layout_dir", None))
         self.model.setup_kv_cache(self.max_batch, self.cache_len, self.device)
 
     def compile(self, serialize_base_path: str) -> None:
@@ -226,6 +231,10 @@ class LlamaForCausalLMInference:
         if rank == 0 and (not dist.is_initialized() or ps.get_data_parallel_rank() == 0):
             self.config.save_pretrained(serialize_base_path)
             self.model_config.save_pretrained(serialize_base_path)
+            if getattr(self, "weight_layouts", None) is not None:
+                from ..trace.weight_layout import save_layouts
+
+                save_layouts(serialize_base_path, self.weight_layouts)
         if dist.is_initialized():
             dist.barrier()
 
@@ -236,6 +245,7 @@ class LlamaForCausalLMInference:
         config = InferenceConfig.from_pretrained(serialize_base_path)
         model_config = cls._config_from_dir(serialize_base_path)
         self = cls(model_config, config, dtype, init_weights=False)
+        self._layout_dir = serialize_base_path      # reuse the compiled weight-layout map, if any
         rank = ps.get_tensor_model_parallel_rank()
         local = load_file(os.path.join(serialize_base_path, f"tp{rank}_sharded_checkpoint.safetensors"))
         self._load_local(local)

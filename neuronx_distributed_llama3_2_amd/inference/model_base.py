@@ -274,7 +274,9 @@ class DecoderInferenceMixin:
         M = x.numel() // x.shape[-1]
         if w.dtype == torch.int8 or (M <= 8 and x.is_cuda):
             return skinny_linear(x, w, scale, b, glu=glu)
-        y = _linear(x, w, b)
+        from ..trace.weight_layout import packed_linear
+
+        y = packed_linear(mod, x, w, b)   # pre-packed K-major copy when the layout pass chose it
         return ops.swiglu(y) if glu else y
 
     def _ffn(self, layer, h: torch.Tensor) -> torch.Tensor:

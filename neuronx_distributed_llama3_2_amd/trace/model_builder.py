@@ -52,6 +52,19 @@ class ModelContainer:
         self.priority_model_idx = priority_model_idx
 
 
+def _bucket_tokens(example) -> int:
+    """GEMM row count of a bucket: B*S of its first input (ids [B, S], or [B, S, H] activations)."""
+    t = example[0]
+    if t.dim() >= 3 or t.is_floating_point():
+        shape = t.shape[:-1]
+    else:
+        shape = t.shape
+    n = 1
+    for d in shape:
+        n *= int(d)
+    return max(n, 1)
+
+
 def _build_nxd(rank, world, collection, checkpoint_loader, router, states, use_graph=True):
     dev = worker_device(rank, world) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda" and dist.is_initialized() and dist.get_backend() != "nccl":
@@ -70,6 +83,14 @@ def _build_nxd(rank, world, collection, checkpoint_loader, router, states, use_g
             mod.load_state_dict(shard_state_dict(mod, full, world, rank, strict=False), strict=False)
     for mod in unique.values():
         mod.to(dev).eval()
+    for mc in collection.values():
+        if mc.priority_model_idx is not None:
+            # weight layout chosen at the priority bucket's shapes, shared by every bucket
+            # (reference trace/model_builder.py:457-586)
+            from .weight_layout import optimize_weight_layout
+
+            mod, _ = mc.model_instance.get(0)
+            optimize_weight_layout(mod, _bucket_tokens(mc.example_inputs[mc.priority_model_idx]))
     state_init = StateInitializer(*states, tp_degree=world, device=dev) if states else None
     nxd = NxDModel(models, tp_degree=world, router=router, state_initializer=state_init)
     with torch.no_grad():

@@ -218,3 +218,23 @@ def test_fused_decode_matches_unfused(hidden, heads):
     lf = f.model.forward_tokens(last, pos, sid, clen).float()
     lu = u.model.forward_tokens(last, pos, sid, clen).float()
     assert ((lf - lu).abs().max() / lu.abs().max()).item() < 3e-2
+
+
+def test_weight_layout_pass_on_gpu(hf_sd):
+    """Measured layout pass at the prefill size: every weight gets a layout, packed copies are
+    K-major, and prefill logits match the stored-layout model (forced-packed too)."""
+    from neuronx_distributed_llama3_2_amd.trace import weight_layout as wl
+
+    cfg, sd = hf_sd
+    m = _model(cfg, sd, torch.bfloat16, device=torch.device("cuda"))
+    torch.manual_seed(3)
+    ids = torch.randint(3, cfg.vocab_size, (2, 100))
+    ref = m._context_encode(ids).cpu()
+    layouts = wl.choose_layouts(m.model, 256)
+    names = [n for n, _ in wl._weights(m.model)]
+    assert set(layouts) == set(names) and set(layouts.values()) <= {"nk", "kn"}
+    for forced in (layouts, {n: "kn" for n in names}):
+        wl.apply_layouts(m.model, forced)
+        out = m._context_encode(ids).cpu()
+        err = (out - ref).abs().max() / ref.abs().max()
+        assert err < 1e-2, err
