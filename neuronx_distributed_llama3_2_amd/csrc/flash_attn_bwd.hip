@@ -42,6 +42,7 @@ constexpr int kWaves = 4;
 constexpr int kThreads = 256;
 constexpr int kBlockK = 256;  // keys per key block (64 per wave)
 constexpr int kBlockQ = 32;   // query rows per tile
+constexpr int kPipeDq = 3;    // dQ operand reads ahead (one MFMA per step)
 
 struct BwdParams {
   const uint16_t* q;
@@ -64,7 +65,7 @@ struct BwdParams {
   int chunk;   // max (q head, q tile) iterations per work item
   int xcd_map; // 0: contiguous item ranges per XCD, 2: interleaved (see bwd_kernel)
   int ablate;  // timing-only ablations (NXD_FAB_ABLATE; outputs wrong): 1 no dQ atomics,
-               // 2 no dK/dV atomics, 4 no dQ MFMAs, 8 no dV/dK MFMAs, 16 no Q/dO tile loads,
+               // 2 no dK/dV atomics, 8 no dV/dK MFMAs, 16 no Q/dO tile loads,
                // 32 no per-tile barriers
 };
 
@@ -133,8 +134,11 @@ __device__ __forceinline__ void mfma_acc_agpr(f32x16_t& acc, const TA& a, const 
   asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-template <int D>
+// PIPE: S / dP operand reads issued this many steps ahead of their MFMAs; PIPE_DVDK: the same for
+// the dV / dK transposed reads (the first ones go out before the softmax VALU)
+template <int D, int PIPE, int PIPE_DVDK>
 __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
+  constexpr int kPipe = PIPE;
   constexpr int CH = D / 8;
   constexpr int KS = D / 16;
   constexpr int NDB = D / 32;
@@ -187,6 +191,8 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
   qstart = (qstart / kBlockQ) * kBlockQ;
   const int n_qt = (p.Sq - qstart + kBlockQ - 1) / kBlockQ;
 
+  // (w stays a VGPR value: made scalar, its uniform branches split the tile body into blocks and
+  // the allocator spills the V rows)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int gi = lane & 15, tq = gi >> 2, tp = gi & 3, g = lane >> 4;
@@ -230,17 +236,19 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
   const int kr0 = (w / NDB) * KEYS_PER_DQ; // dQ: this wave's first key of the block
   // (image bases are folded into the registers: ds_read immediates are 16-bit)
   const uint32_t L0 = lds_addr(smem);
-  uint32_t a_q[KS], a_do[KS], a_krow[KS], a_vrow[KS];  // row reads: q/dO row r, K row 64w+r, V row 32w+r
-  uint32_t a_trq[2][NDB], a_trd[2][NDB];               // tr reads rows 4hh+tq+8j, col 32dbk+16(g&1)+4tp
+  // row reads of q/dO row r, K row 64w+r, V row 32w+r all use a_q (the dO image is a constant
+  // away; K / V a wave-uniform SGPR away, added per read so the registers are not replicated)
+  uint32_t a_q[KS];
+  uint32_t a_trq[2][NDB];                  // tr reads rows 4hh+tq+8j, col 32dbk+16(g&1)+4tp (Q; dO +const)
+  const uint32_t kofs0 = __builtin_amdgcn_readfirstlane((uint32_t)(OFF_K - OFF_Q + 64 * w * (2 * D)));
+  const uint32_t vofs0 = __builtin_amdgcn_readfirstlane((uint32_t)(OFF_V - OFF_Q + 32 * w * (2 * D)));
+  constexpr int DO_Q = OFF_DO - OFF_Q;
   uint32_t a_dsw[4];                       // dS^T writes: key 64w+r, q 8gq+4hh
   uint32_t a_dsr[2], a_ktr[2];             // dQ tr reads: dS^T keys kr0+8hh+tq+4j / K rows
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int a_row = lds_off<D>(r, 2 * s + hh);
     a_q[s] = L0 + OFF_Q + a_row;
-    a_do[s] = L0 + OFF_DO + a_row;
-    a_krow[s] = L0 + OFF_K + 64 * w * (2 * D) + a_row;
-    a_vrow[s] = L0 + OFF_V + 32 * w * (2 * D) + a_row;
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -249,7 +257,6 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
       const int col = 32 * dbk + 16 * (g & 1) + 4 * tp;
       const int a_tr = lds_off<D>(4 * hh + tq + 8 * j, col >> 3) + (col & 7) * 2;
       a_trq[j][dbk] = L0 + OFF_Q + a_tr;
-      a_trd[j][dbk] = L0 + OFF_DO + a_tr;
     }
 #pragma unroll
   for (int gq = 0; gq < 4; ++gq) a_dsw[gq] = L0 + OFF_DS + 64 * w * 64 + ds_off(r, 8 * gq + 4 * hh);
@@ -264,12 +271,12 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
   // v_add back into the loop (the big constants do not fit the 16-bit ds offset)
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    asm volatile("" : "+v"(a_q[s]), "+v"(a_do[s]), "+v"(a_krow[s]), "+v"(a_vrow[s]));
+    asm volatile("" : "+v"(a_q[s]));
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
 #pragma unroll
-    for (int dbk = 0; dbk < NDB; ++dbk) asm volatile("" : "+v"(a_trq[j][dbk]), "+v"(a_trd[j][dbk]));
+    for (int dbk = 0; dbk < NDB; ++dbk) asm volatile("" : "+v"(a_trq[j][dbk]));
     asm volatile("" : "+v"(a_dsr[j]), "+v"(a_ktr[j]));
   }
 #pragma unroll
@@ -287,6 +294,21 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
     do_lane[i] = row * (int)p.do_ss + ch * 8;
   }
 
+  // Q / dO tile + row constants -> LDS by LDS-DMA (global_load_lds), one tile ahead into the other
+  // buffer.  Issued from inline asm: when the compiler sees an LDS-DMA in flight it waits for it
+  // (vmcnt(0)) before every transposed LDS read, which exposed the whole prefetch once per tile.
+  // Completion is tracked by hand (the counted vmcnt wait at the end of each tile).  M0 carries the
+  // wave-uniform LDS destination and is restored after the issue.
+  auto dma16 = [&](const void* src, uint32_t lds_dst) {
+    uint32_t sv;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(sv) : "v"(src), "s"(lds_dst) : "memory");
+  };
+  auto dma4 = [&](const void* src, uint32_t lds_dst) {
+    uint32_t sv;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(sv) : "v"(src), "s"(lds_dst) : "memory");
+  };
   auto issue_tile = [&](int it, int buf) {
     const int hq = hkv * G + it / n_qt;
     const int qt0 = qstart + (it % n_qt) * kBlockQ;
@@ -303,16 +325,13 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
         qo = rr * (int)p.q_ss + ch * 8;
         dof = rr * (int)p.do_ss + ch * 8;
       }
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(qb + qo),
-                                       (__attribute__((address_space(3))) void*)(smem + OFF_Q + buf * QT_BYTES + piece * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(db + dof),
-                                       (__attribute__((address_space(3))) void*)(smem + OFF_DO + buf * QT_BYTES + piece * 1024), 16, 0, 0);
+      dma16(qb + qo, __builtin_amdgcn_readfirstlane(L0 + OFF_Q + buf * QT_BYTES + piece * 1024));
+      dma16(db + dof, __builtin_amdgcn_readfirstlane(L0 + OFF_DO + buf * QT_BYTES + piece * 1024));
     }
     if (w == 0) {
       const int qi = min(qt0 + (lane & 31), p.Sq - 1);
       const float* src = (lane < 32 ? p.nlse : p.ndelta) + ((int64_t)b * p.Hq + hq) * p.Sq + qi;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(smem + OFF_LD + buf * 256), 4, 0, 0);
+      dma4(src, __builtin_amdgcn_readfirstlane(L0 + OFF_LD + buf * 256));
     }
   };
 
@@ -338,13 +357,18 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
     const int qt0 = qstart + (it % n_qt) * kBlockQ;
     // buffer buf^1 was last read in the previous tile, closed by its final barrier
     if (it + 1 < it_end && !(p.ablate & 16)) issue_tile(it + 1, buf ^ 1);
+    uint32_t kofs = kofs0, vofs = vofs0;
+    asm volatile("" : "+s"(kofs), "+s"(vofs));  // per tile: the adds stay next to their reads
     const int qlast = qt0 + kBlockQ - 1 + p.causal_offset;  // last key any row of the tile may see
 
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int kc0 = wkey0 + 32 * c;
-      if (!p.causal || kc0 <= qlast) {
-        touched[c] = true;
+      // no branch on the causal diagonal: a fully masked column computes P = dS = 0 (the tile's
+      // time is set by wave 0, whose columns are never fully masked), and a branch around MFMAs
+      // would need to be a uniform jump -- an MFMA ignores EXEC
+      touched[c] = touched[c] || !p.causal || kc0 <= qlast;
+      {
         // ---- S = Q K^T - LSE/scale, dP = dO V^T - delta  (key on the lane; row constants as
         // the initial accumulators)
         f32x16_t s_acc, dp_acc;
@@ -358,20 +382,44 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
             dp_acc[4 * gq + i] = d4[i];
           }
         }
+        // operands of step s are read kPipe steps ahead of its MFMAs (explicit software pipeline:
+        // each step is fenced for the scheduler, so a read is never sunk next to its consumer and
+        // the MFMAs wait only for their own operands -- lgkmcnt(N), not lgkmcnt(0))
+        u32x4_t qa[KS], kk[KS], da[KS];
+        bf16x8_t vb[KS];
+        auto ld_sdp = [&](int s) {
+          qa[s] = lds_ld<u32x4_t>(a_q[s] + QB);
+          kk[s] = lds_ld<u32x4_t>(a_q[s] + kofs + c * 32 * (2 * D));
+          da[s] = lds_ld<u32x4_t>(a_q[s] + DO_Q + DB);
+          if (c == 0)
+            vb[s] = vf[s];
+          else
+            vb[s] = __builtin_bit_cast(bf16x8_t, lds_ld<u32x4_t>(a_q[s] + vofs));
+        };
+#pragma unroll
+        for (int s = 0; s < kPipe; ++s) ld_sdp(s);
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-          const u32x4_t qa = lds_ld<u32x4_t>(a_q[s] + QB);
-          const u32x4_t kk = lds_ld<u32x4_t>(a_krow[s] + c * 32 * (2 * D));
-          const u32x4_t da = lds_ld<u32x4_t>(a_do[s] + DB);
-          s_acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, qa), __builtin_bit_cast(bf16x8_t, kk), s_acc, 0, 0, 0);
-          bf16x8_t vb;
-          if (c == 0) {
-            vb = vf[s];
-          } else {
-            vb = __builtin_bit_cast(bf16x8_t, lds_ld<u32x4_t>(a_vrow[s]));
-          }
-          dp_acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, da), vb, dp_acc, 0, 0, 0);
+          if (s + kPipe < KS) ld_sdp(s + kPipe);
+          s_acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, qa[s]), __builtin_bit_cast(bf16x8_t, kk[s]), s_acc, 0, 0, 0);
+          dp_acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, da[s]), vb[s], dp_acc, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
         }
+        // first dV / dK operands (transposed dO / Q reads) go out before the softmax VALU
+        short4_t tr_lo[2 * NDB][2], tr_hi[2 * NDB][2];
+        auto ld_dvdk = [&](int st) {
+          const int s2 = st / NDB, dbk = st % NDB;
+          const int o = s2 * 16 * (2 * D);
+          tr_lo[st][0] = lds_tr(a_trq[0][dbk] + DO_Q + DB + o);
+          tr_hi[st][0] = lds_tr(a_trq[1][dbk] + DO_Q + DB + o);
+          tr_lo[st][1] = lds_tr(a_trq[0][dbk] + QB + o);
+          tr_hi[st][1] = lds_tr(a_trq[1][dbk] + QB + o);
+        };
+        if (!(p.ablate & 8)) {
+#pragma unroll
+          for (int st = 0; st < PIPE_DVDK; ++st) ld_dvdk(st);
+        }
+        __builtin_amdgcn_sched_barrier(0);
         // ---- P, dS (element e of the lane: query row 8(e>>2) + 4hh + (e&3), key kc0 + r)
         const bool need_mask = (p.causal && kc0 + 31 > qt0 + p.causal_offset) || qt0 + kBlockQ > p.Sq || kc0 + 32 > p.Sk;
         bf16x8_t pf[2], dsf[2];
@@ -405,24 +453,18 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
         // ---- dV += P^T dO ; dK += dS^T Q   (B operands by transposed reads of the tile images)
         if (!(p.ablate & 8)) {
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-            for (int dbk = 0; dbk < NDB; ++dbk) {
-              const int o = s2 * 16 * (2 * D);
-              const short4_t dlo = lds_tr(a_trd[0][dbk] + DB + o);
-              const short4_t dhi = lds_tr(a_trd[1][dbk] + DB + o);
-              const bf16s8_t db8 = {dlo[0], dlo[1], dlo[2], dlo[3], dhi[0], dhi[1], dhi[2], dhi[3]};
-              mfma_acc_agpr(acc_dv[c][dbk], pf[s2], db8);
-              const short4_t qlo = lds_tr(a_trq[0][dbk] + QB + o);
-              const short4_t qhi = lds_tr(a_trq[1][dbk] + QB + o);
-              const bf16s8_t qb8 = {qlo[0], qlo[1], qlo[2], qlo[3], qhi[0], qhi[1], qhi[2], qhi[3]};
-              mfma_acc_agpr(acc_dk[c][dbk], dsf[s2], qb8);
-            }
+          for (int st = 0; st < 2 * NDB; ++st) {
+            if (st + PIPE_DVDK < 2 * NDB) ld_dvdk(st + PIPE_DVDK);
+            const int s2 = st / NDB, dbk = st % NDB;
+            const bf16s8_t db8 = {tr_lo[st][0][0], tr_lo[st][0][1], tr_lo[st][0][2], tr_lo[st][0][3],
+                                  tr_hi[st][0][0], tr_hi[st][0][1], tr_hi[st][0][2], tr_hi[st][0][3]};
+            const bf16s8_t qb8 = {tr_lo[st][1][0], tr_lo[st][1][1], tr_lo[st][1][2], tr_lo[st][1][3],
+                                  tr_hi[st][1][0], tr_hi[st][1][1], tr_hi[st][1][2], tr_hi[st][1][3]};
+            mfma_acc_agpr(acc_dv[c][dbk], pf[s2], db8);
+            mfma_acc_agpr(acc_dk[c][dbk], dsf[s2], qb8);
+            __builtin_amdgcn_sched_barrier(0);
           }
         }
-      } else {
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) lds_st(a_dsw[gq] + c * 32 * 64, u32x2_t{0, 0});
       }
     }
     // dS^T complete.  Raw barrier: the tile prefetch (LDS-DMA) stays in flight across it.
@@ -430,29 +472,34 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
     if (!(p.ablate & 32)) __builtin_amdgcn_s_barrier();
 
     // ---- dQ[q][d] += dS[q][key] K[key][d] over this wave's (d block, key range)
-    int nks = KEYS_PER_DQ / 16;  // key groups of 16 that hold any unmasked key
-    if (p.causal) nks = max(0, min(nks, (qlast - (kb0 + kr0) + 16) / 16));
-    if (p.ablate & 4) nks = 0;
+    // all key groups, masked ones included (their dS^T entries are zeros): unguarded MFMAs, and
+    // near-diagonal tiles only
     // two independent accumulation chains (even / odd key groups): a single chain of dependent
     // 32x32 MFMAs runs at half rate
     f32x16_t acc_dq = f32x16_t{0}, acc_dq2 = f32x16_t{0};
+    constexpr int NKS = KEYS_PER_DQ / 16;
+    short4_t qa0[NKS], qa1[NKS], qb0[NKS], qb1[NKS];
+    auto ld_dq = [&](int s) {
+      qa0[s] = lds_tr(a_dsr[0] + s * 16 * 64);
+      qa1[s] = lds_tr(a_dsr[1] + s * 16 * 64);
+      qb0[s] = lds_tr(a_ktr[0] + s * 16 * (2 * D));
+      qb1[s] = lds_tr(a_ktr[1] + s * 16 * (2 * D));
+    };
 #pragma unroll
-    for (int s = 0; s < KEYS_PER_DQ / 16; ++s) {
-      if (s < nks) {
-        const short4_t a0 = lds_tr(a_dsr[0] + s * 16 * 64);
-        const short4_t a1 = lds_tr(a_dsr[1] + s * 16 * 64);
-        const bf16s8_t a8 = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-        const short4_t b0 = lds_tr(a_ktr[0] + s * 16 * (2 * D));
-        const short4_t b1 = lds_tr(a_ktr[1] + s * 16 * (2 * D));
-        const bf16s8_t b8 = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-        if (s & 1)
-          acc_dq2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a8), __builtin_bit_cast(bf16x8_t, b8), acc_dq2, 0, 0, 0);
-        else
-          acc_dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a8), __builtin_bit_cast(bf16x8_t, b8), acc_dq, 0, 0, 0);
-      }
+    for (int s = 0; s < kPipeDq; ++s) ld_dq(s);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      if (s + kPipeDq < NKS) ld_dq(s + kPipeDq);
+      const bf16s8_t a8 = {qa0[s][0], qa0[s][1], qa0[s][2], qa0[s][3], qa1[s][0], qa1[s][1], qa1[s][2], qa1[s][3]};
+      const bf16s8_t b8 = {qb0[s][0], qb0[s][1], qb0[s][2], qb0[s][3], qb1[s][0], qb1[s][1], qb1[s][2], qb1[s][3]};
+      if (s & 1)
+        acc_dq2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a8), __builtin_bit_cast(bf16x8_t, b8), acc_dq2, 0, 0, 0);
+      else
+        acc_dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a8), __builtin_bit_cast(bf16x8_t, b8), acc_dq, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     acc_dq += acc_dq2;
-    bool adder = nks > 0 && !(p.ablate & 1);
+    bool adder = !(p.ablate & 1);
     if constexpr (KEY_SPLIT == 2) {
       // key-half 1 hands its partial to key-half 0 through LDS (no doubled atomics)
       float* red = reinterpret_cast<float*>(smem + OFF_RED) + (dbq * 64 + lane) * 16;
@@ -475,8 +522,7 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
       }
     }
     if (adder) {
-      // 16 UNCONDITIONAL atomics per lane (dq_acc has Sq padded to kBlockQ rows), so the
-      // counted wait below knows exactly how many of this wave's VM ops are atomics.
+      // (dq_acc has Sq padded to kBlockQ rows: no bounds checks)
       float* dqb = p.dq_acc + (((int64_t)b * p.Hq + hq) * Sq_pad + qt0 + 4 * hh) * D + 32 * dbq + r;
 #pragma unroll
       for (int e = 0; e < 16; ++e) atomicAdd(dqb + ((e & 3) + 8 * (e >> 2)) * D, acc_dq[e]);
@@ -676,12 +722,32 @@ int chunk_override() {
   return g_chunk;
 }
 
+static int g_pipe = -1;
+int pipe_variant() {
+  if (g_pipe < 0) {
+    const char* e = getenv("NXD_FAB_PIPE");
+    g_pipe = e ? atoi(e) : 12;
+  }
+  return g_pipe;
+}
+
+template <int D, int PIPE, int PIPE_DVDK>
+void launch_bwd(const BwdParams& p, int64_t items, size_t lds, hipStream_t stream) {
+  static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per instantiation
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)bwd_kernel<D, PIPE, PIPE_DVDK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((bwd_kernel<D, PIPE, PIPE_DVDK>), dim3((unsigned)items), dim3(kThreads), lds, stream, p);
+}
+
 }  // namespace fab
 
 void flash_attn_bwd_set_knob(int which, int value) {
   if (which == 0) fab::g_ablate = value;
   if (which == 1) fab::g_chunk = value;
   if (which == 3) fab::g_xcd = value;
+  if (which == 4) fab::g_pipe = value;  // pipeline depths: 12 (default), 11, 21, 0
 }
 
 // fp32 workspace floats the backward needs: dq_acc + dk_acc + dv_acc + nlse + ndelta
@@ -743,20 +809,15 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   if (items > 0) {
     if (D == 128) {
       const size_t lds = kBlockK * 128 * 2 + 4 * kBlockQ * 128 * 2 + kBlockK * 64 + 512 + 128 * 128 * 2;
-      static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once
-      if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)bwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_set = true;
+      switch (pipe_variant()) {
+        case 11: launch_bwd<128, 1, 1>(p, items, lds, stream); break;
+        case 21: launch_bwd<128, 2, 1>(p, items, lds, stream); break;
+        case 0: launch_bwd<128, 0, 0>(p, items, lds, stream); break;
+        default: launch_bwd<128, 1, 2>(p, items, lds, stream); break;
       }
-      hipLaunchKernelGGL(bwd_kernel<128>, dim3((unsigned)items), dim3(kThreads), lds, stream, p);
     } else {
       const size_t lds = kBlockK * 64 * 2 + 4 * kBlockQ * 64 * 2 + kBlockK * 64 + 512 + 2 * 64 * 16 * 4 + 128 * 64 * 2;
-      static bool attr_set = false;
-      if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)bwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_set = true;
-      }
-      hipLaunchKernelGGL(bwd_kernel<64>, dim3((unsigned)items), dim3(kThreads), lds, stream, p);
+      launch_bwd<64, 1, 2>(p, items, lds, stream);
     }
   }
   if (D == 128) {
