@@ -65,7 +65,7 @@ struct BwdParams {
   int chunk;   // max (q head, q tile) iterations per work item
   int xcd_map; // 0: contiguous item ranges per XCD, 2: interleaved (see bwd_kernel)
   int ablate;  // timing-only ablations (NXD_FAB_ABLATE; outputs wrong): 1 no dQ atomics,
-               // 2 no dK/dV atomics, 8 no dV/dK MFMAs, 16 no Q/dO tile loads,
+               // 2 no dK/dV atomics, 16 no Q/dO tile loads,
                // 32 no per-tile barriers
 };
 
@@ -415,45 +415,43 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
           tr_lo[st][1] = lds_tr(a_trq[0][dbk] + QB + o);
           tr_hi[st][1] = lds_tr(a_trq[1][dbk] + QB + o);
         };
-        if (!(p.ablate & 8)) {
 #pragma unroll
-          for (int st = 0; st < PIPE_DVDK; ++st) ld_dvdk(st);
-        }
+        for (int st = 0; st < PIPE_DVDK; ++st) ld_dvdk(st);
         __builtin_amdgcn_sched_barrier(0);
-        // ---- P, dS (element e of the lane: query row 8(e>>2) + 4hh + (e&3), key kc0 + r)
+        // ---- P, dS (element e of the lane: query row 8(e>>2) + 4hh + (e&3), key kc0 + r).  Rows
+        // 0-15 (half 0) first; the exps of half 1 run in the shadow of half 0's dV / dK MFMAs.
         const bool need_mask = (p.causal && kc0 + 31 > qt0 + p.causal_offset) || qt0 + kBlockQ > p.Sq || kc0 + 32 > p.Sk;
+        float pv[16];
         bf16x8_t pf[2], dsf[2];
-        if (!need_mask) {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const float pv = __builtin_amdgcn_exp2f(s_acc[e] * p.scale_log2);
-            pf[e >> 3][e & 7] = (__bf16)pv;
-            dsf[e >> 3][e & 7] = (__bf16)(pv * dp_acc[e]);
-          }
-        } else {
+        auto p_fix = [&](int e0) {  // masked tiles only (a VALU-only exec-masked block)
           const int my_key = kc0 + r;
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            float pv = __builtin_amdgcn_exp2f(s_acc[e] * p.scale_log2);
+          for (int e = e0; e < e0 + 8; ++e) {
             const int qg = qt0 + 8 * (e >> 2) + 4 * hh + (e & 3);
             const bool bad = qg >= p.Sq || my_key >= p.Sk || (p.causal && my_key > qg + p.causal_offset);
-            pv = bad ? 0.f : pv;
-            pf[e >> 3][e & 7] = (__bf16)pv;
-            dsf[e >> 3][e & 7] = (__bf16)(pv * dp_acc[e]);
+            pv[e] = bad ? 0.f : pv[e];
           }
-        }
-        // ---- dS -> LDS (transposed image [key][q]); whole-vector bit casts (per-element
-        // extraction of bf16 ext_vectors miscompiles on ROCm 7.2)
-        const u32x4_t ds_w0 = __builtin_bit_cast(u32x4_t, dsf[0]);
-        const u32x4_t ds_w1 = __builtin_bit_cast(u32x4_t, dsf[1]);
-        lds_st(a_dsw[0] + c * 32 * 64, u32x2_t{ds_w0[0], ds_w0[1]});
-        lds_st(a_dsw[1] + c * 32 * 64, u32x2_t{ds_w0[2], ds_w0[3]});
-        lds_st(a_dsw[2] + c * 32 * 64, u32x2_t{ds_w1[0], ds_w1[1]});
-        lds_st(a_dsw[3] + c * 32 * 64, u32x2_t{ds_w1[2], ds_w1[3]});
-        // ---- dV += P^T dO ; dK += dS^T Q   (B operands by transposed reads of the tile images)
-        if (!(p.ablate & 8)) {
+        };
+        auto p_half = [&](int h) {  // bf16 P / dS of half h, dS^T rows -> LDS
 #pragma unroll
-          for (int st = 0; st < 2 * NDB; ++st) {
+          for (int j = 0; j < 8; ++j) {
+            pf[h][j] = (__bf16)pv[8 * h + j];
+            dsf[h][j] = (__bf16)(pv[8 * h + j] * dp_acc[8 * h + j]);
+          }
+          // whole-vector bit casts (per-element extraction of bf16 ext_vectors miscompiles on ROCm 7.2)
+          const u32x4_t dw = __builtin_bit_cast(u32x4_t, dsf[h]);
+          lds_st(a_dsw[2 * h] + c * 32 * 64, u32x2_t{dw[0], dw[1]});
+          lds_st(a_dsw[2 * h + 1] + c * 32 * 64, u32x2_t{dw[2], dw[3]});
+        };
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pv[e] = __builtin_amdgcn_exp2f(s_acc[e] * p.scale_log2);
+        if (need_mask) p_fix(0);
+        p_half(0);
+        // ---- dV += P^T dO ; dK += dS^T Q   (B operands by transposed reads of the tile images)
+        constexpr int EPS = 8 / NDB;  // half-1 exps per half-0 step
+#pragma unroll
+        for (int st = 0; st < 2 * NDB; ++st) {
+          {
             if (st + PIPE_DVDK < 2 * NDB) ld_dvdk(st + PIPE_DVDK);
             const int s2 = st / NDB, dbk = st % NDB;
             const bf16s8_t db8 = {tr_lo[st][0][0], tr_lo[st][0][1], tr_lo[st][0][2], tr_lo[st][0][3],
@@ -462,6 +460,15 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
                                   tr_hi[st][1][0], tr_hi[st][1][1], tr_hi[st][1][2], tr_hi[st][1][3]};
             mfma_acc_agpr(acc_dv[c][dbk], pf[s2], db8);
             mfma_acc_agpr(acc_dk[c][dbk], dsf[s2], qb8);
+          }
+          if (st < NDB) {
+#pragma unroll
+            for (int j = 0; j < EPS; ++j) pv[8 + EPS * st + j] = __builtin_amdgcn_exp2f(s_acc[8 + EPS * st + j] * p.scale_log2);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (st == NDB - 1) {
+            if (need_mask) p_fix(8);
+            p_half(1);
             __builtin_amdgcn_sched_barrier(0);
           }
         }

@@ -12,9 +12,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from neuronx_distributed_llama3_2_amd import ops  # noqa: E402
 
-VARIANTS = {"full": 0, "no_dq_atomics": 1, "no_dkdv_atomics": 2, "no_atomics": 3, "no_dq_mfma": 5,
-            "no_dvdk_mfma": 8, "only_s_dp": 15,
-            "no_tile_loads": 16, "no_barriers": 32, "only_s_dp_no_loads": 31, "only_s_dp_no_loads_no_bar": 63}
+VARIANTS = {"full": 0, "no_dq_atomics": 1, "no_dkdv_atomics": 2, "no_atomics": 3, "no_tile_loads": 16,
+            "no_barriers": 32, "no_loads_no_bar": 48, "no_atomics_loads_bar": 51}
 
 
 def main():
