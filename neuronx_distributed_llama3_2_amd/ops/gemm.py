@@ -54,9 +54,11 @@ _WGRAD_BF16 = os.environ.get("NXD_WGRAD_BF16", "0") == "1"
 _scratch = {}
 
 
-# wgrad through transposed operands pays when the GEMM time saved, ~0.39e-15 * T*N*K s, beats the
-# two transposes, ~0.8e-12 * T*(N+K) s: N*K/(N+K) above ~2200 (Llama-3-8B: gate_up, down, qkv and
-# lm_head at TP=1; none of the TP=8 shards).  NXD_WGRAD_T=0 disables, =2 forces.
+# wgrad through transposed operands pays when the GEMM time saved beats the two transposes
+# (~0.8e-12 * T*(N+K) s): measured, N*K/(N+K) above ~1200 -- Llama-3-8B gate_up, down, qkv and
+# lm_head at TP=1; gate_up (975 -> 1116 TF/s), down (920 -> 944) and lm_head at TP=8, but not the
+# TP=8 qkv / o shards (798 -> 566, 742 -> 440; profiles/r2_gemm_tp8_wgrad_layouts.jsonl).
+# NXD_WGRAD_T=0 disables, =2 forces.
 _WGRAD_T = os.environ.get("NXD_WGRAD_T", "1")
 
 
@@ -66,7 +68,7 @@ def _use_wgrad_t(go2: torch.Tensor, x2: torch.Tensor) -> bool:
     T, N, K = go2.shape[0], go2.shape[1], x2.shape[1]
     if T % 8 or N % 8 or K % 8 or go2.stride(-1) != 1 or x2.stride(-1) != 1 or go2.stride(0) % 8 or x2.stride(0) % 8:
         return False
-    return _WGRAD_T == "2" or N * K / (N + K) > 2200
+    return _WGRAD_T == "2" or N * K / (N + K) > 1200
 
 
 def _wgrad_scratch(n: int, dtype, device, tag: str = "") -> torch.Tensor:
