@@ -3,7 +3,9 @@
 Config (BASELINE.json): Llama-3-8B architecture (random init, synthetic token data), sequence
 length 8192, micro-batch 1, tensor parallel TP = N (<= 8) with sequence parallelism, flash
 attention, fp32 master weights + fused AdamW (ZeRO-1 when DP > 1), gradient accumulation up to the
-global batch.  `--parallelism dp` instead runs TP=1 x DP=N (weak scaling).
+global batch.  `--parallelism dp` instead runs TP=1 x DP=N (weak scaling).  `--pp P` runs the
+BASELINE's pipeline config: TP = N / P x PP = P through NxDPPModel's 1F1B schedule (P2P over RCCL
+on a side stream), global batch 32 by default (the 1F1B bubble is (P-1)/(M+P-1) for M micro-batches).
 
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
@@ -28,6 +30,8 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# library log records go to stderr: stdout carries exactly one line, the JSON result
+os.environ.setdefault("NXD_LOG_STREAM", "stderr")
 
 # Micro-batch per TP degree: TP shrinks every per-rank GEMM and the attention head count, so the
 # TP=4/8 ranks process several sequences per micro-batch to keep MFMA tiles and the attention grid
@@ -48,7 +52,8 @@ def parse():
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--mbs", type=int, default=None,
                     help="micro-batch size (sequences); default per TP degree (MBS_BY_TP)")
-    ap.add_argument("--gbs", type=int, default=8, help="global batch (sequences per optimizer step)")
+    ap.add_argument("--gbs", type=int, default=None, help="global batch (sequences per optimizer step); 8 (32 with --pp)")
+    ap.add_argument("--pp", type=int, default=1, help="pipeline stages (NxDPPModel 1F1B); TP = N / pp")
     ap.add_argument("--parallelism", choices=["tp", "dp"], default="tp")
     ap.add_argument("--layers", type=int, default=None, help="override #layers (NOT the headline config)")
     ap.add_argument("--no-sp", action="store_true")
@@ -92,6 +97,33 @@ def launch_local_ranks(argv, n: int) -> int:
     return rc
 
 
+def _build_pipeline(a, cfg, tp, n_micro, dev, dtype):
+    """NxDPPModel (1F1B over `n_micro` micro-batches, even layer split) + the trainer's optimizer
+    (fp32 master weights, ZeRO-1 over DP) through the public training API."""
+    import torch
+
+    import neuronx_distributed_llama3_2_amd as nxd
+    from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaDecoderLayer, LlamaForCausalLM
+    from neuronx_distributed_llama3_2_amd.parallel_layers import parallel_state as ps
+    from neuronx_distributed_llama3_2_amd.utils.training_utils import create_partition, get_param_groups_by_weight_decay
+
+    cuts = create_partition(cfg.num_hidden_layers, a.pp)
+    pcfg = {"transformer_layer_cls": LlamaDecoderLayer, "num_microbatches": n_micro, "virtual_pipeline_size": 1,
+            "input_names": ["input_ids", "labels"], "broadcast_and_average_loss": True,
+            "auto_partition": False, "pipeline_cuts": cuts}
+    nxd_config = nxd.neuronx_distributed_config(
+        tensor_parallel_size=tp, pipeline_parallel_size=a.pp, pipeline_config=pcfg,
+        sequence_parallel=cfg.sequence_parallel_enabled,
+        optimizer_config={"zero_one_enabled": True, "grad_clipping": True, "max_grad_norm": 1.0},
+        mixed_precision_config={"use_master_weights": True, "use_fp32_grad_acc": True,
+                                "use_master_weights_in_ckpt": False})
+    model = nxd.initialize_parallel_model(nxd_config, LlamaForCausalLM, cfg, dtype=dtype, device=dev)
+    groups = get_param_groups_by_weight_decay(model, 0.01)
+    opt = nxd.initialize_parallel_optimizer(nxd_config, torch.optim.AdamW, groups, lr=1e-5, betas=(0.9, 0.95), eps=1e-8)
+    assert ps.get_pipeline_model_parallel_size() == a.pp
+    return model, opt
+
+
 def main(a):
     import torch
     import torch.distributed as dist
@@ -132,9 +164,19 @@ def main(a):
     if comm_world != world:
         raise SystemExit(f"bench: {backend} all-reduce saw {comm_world} ranks, expected {world}")
 
-    tp = min(world, 8) if a.parallelism == "tp" else 1
-    ps.initialize_model_parallel(tensor_model_parallel_size=tp)
-    dp = ps.get_data_parallel_size()
+    if a.gbs is None:
+        a.gbs = 32 if a.pp > 1 else 8
+    if a.pp > 1:
+        if world % a.pp or a.parallelism != "tp":
+            raise SystemExit(f"bench: --pp {a.pp} needs --parallelism tp and a GPU count divisible by it")
+        tp = min(world // a.pp, 8)
+    else:
+        tp = min(world, 8) if a.parallelism == "tp" else 1
+    if a.pp == 1:
+        ps.initialize_model_parallel(tensor_model_parallel_size=tp)
+        dp = ps.get_data_parallel_size()
+    else:
+        dp = world // (tp * a.pp)
     model_parallel_manual_seed(1234)
 
     over = dict(sequence_parallel_enabled=(tp > 1 and not a.no_sp), max_position_embeddings=max(8192, a.seq))
@@ -145,19 +187,23 @@ def main(a):
     elif a.ckpt == "selective":
         over["selective_checkpoint_enabled"] = True
     cfg = llama_config(a.model, **over)
-    model = LlamaForCausalLM(cfg, dtype=torch.bfloat16, device=dev)
-    model.train()
-    nparams_local = sum(p.numel() for p in model.parameters())
-    decay = [p for n, p in model.named_parameters() if p.dim() > 1]
-    no_decay = [p for n, p in model.named_parameters() if p.dim() <= 1]
-    opt = FlatMixedPrecisionAdamW([{"params": decay, "weight_decay": 0.01}, {"params": no_decay, "weight_decay": 0.0}],
-                                  lr=1e-5, betas=(0.9, 0.95), eps=1e-8, zero1=dp > 1, grad_clipping=True,
-                                  max_grad_norm=1.0, shared_param_ids=find_shared_params(model))
     if a.mbs is None:
         a.mbs = max(1, min(MBS_BY_TP.get(tp, 1), a.gbs // dp))
     if a.gbs % (a.mbs * dp):
         raise SystemExit(f"bench: global batch {a.gbs} not divisible by micro-batch {a.mbs} x DP {dp}")
     accum = a.gbs // (a.mbs * dp)
+    if a.pp > 1:
+        model, opt = _build_pipeline(a, cfg, tp, accum, dev, torch.bfloat16)
+        dp = ps.get_data_parallel_size()
+    else:
+        model = LlamaForCausalLM(cfg, dtype=torch.bfloat16, device=dev)
+        model.train()
+        decay = [p for n, p in model.named_parameters() if p.dim() > 1]
+        no_decay = [p for n, p in model.named_parameters() if p.dim() <= 1]
+        opt = FlatMixedPrecisionAdamW([{"params": decay, "weight_decay": 0.01}, {"params": no_decay, "weight_decay": 0.0}],
+                                      lr=1e-5, betas=(0.9, 0.95), eps=1e-8, zero1=dp > 1, grad_clipping=True,
+                                      max_grad_norm=1.0, shared_param_ids=find_shared_params(model))
+    nparams_local = sum(p.numel() for p in model.parameters())
     # a fresh batch for every micro-step of every step (warmup included), generated before the timed
     # region; identical across the TP ranks of one DP rank, different across DP ranks.  Random tokens
     # cannot be memorised, so the reported loss stays near ln(V) and flags numerics regressions.
@@ -167,6 +213,14 @@ def main(a):
     cursor = [0]
 
     def train_step():
+        if a.pp > 1:
+            # one 1F1B pass over all `accum` micro-batches of this DP rank, then the optimizer step
+            ids = batches[cursor[0]:cursor[0] + accum].reshape(accum * a.mbs, a.seq)
+            cursor[0] += accum
+            loss = model.run_train(input_ids=ids, labels=ids)
+            opt.step()
+            opt.zero_grad()
+            return loss
         for i in range(accum):
             opt.set_grad_sync(i == accum - 1)
             ids = batches[cursor[0]]
@@ -197,9 +251,13 @@ def main(a):
         mem = torch.cuda.max_memory_allocated(dev) / 2**30 if use_cuda else 0.0
         nparams = llama_num_params(cfg)
         fpt = model_flops_per_token(nparams, cfg.num_hidden_layers, cfg.hidden_size, a.seq)
-        par = f"tp{tp}" + ("_sp" if over["sequence_parallel_enabled"] else "") + (f"_dp{dp}_zero1" if dp > 1 else "")
+        par = f"tp{tp}" + ("_sp" if over["sequence_parallel_enabled"] else "") + \
+            (f"_pp{a.pp}_1f1b" if a.pp > 1 else "") + (f"_dp{dp}_zero1" if dp > 1 else "")
+        metric = "tokens/sec (whole node) Llama-3-8B TP=8 bf16 training at 1/2/4/8 MI355X"
+        if a.pp > 1:
+            metric = f"tokens/sec (whole node) Llama-3-8B TP={tp} x PP={a.pp} 1F1B bf16 training"
         rec = {
-            "metric": "tokens/sec (whole node) Llama-3-8B TP=8 bf16 training at 1/2/4/8 MI355X",
+            "metric": metric,
             "value": round(value, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -215,7 +273,7 @@ def main(a):
                        "micro_batch": a.mbs, "seq_len": a.seq, "parallelism": par, "grad_accum": accum,
                        "optimizer": "AdamW fp32-master" + (" ZeRO-1" if dp > 1 else ""),
                        "activation_checkpoint": a.ckpt or "none"},
-            "loss": round(float(loss.item()), 4),
+            "loss": round(float(loss.item() if torch.is_tensor(loss) else loss), 4),
             "comm_backend": backend,
             "comm_world_size": comm_world,
             "params_per_rank": nparams_local,

@@ -1,7 +1,8 @@
 """Rank-aware logging (reference: src/neuronx_distributed/utils/logger.py:16-112).
 
-`NXD_LOG_LEVEL` sets the level (default INFO), `NXD_LOG_HIDE_TIME=1` drops timestamps; by default
-only global rank 0 emits records.
+`NXD_LOG_LEVEL` sets the level (default INFO), `NXD_LOG_HIDE_TIME=1` drops timestamps,
+`NXD_LOG_STREAM=stderr` sends records to stderr instead of stdout (bench.py: stdout carries only its
+JSON result line); by default only global rank 0 emits records.
 """
 
 from __future__ import annotations
@@ -48,7 +49,7 @@ def get_logger(name: str = "neuronx_distributed", rank0_only: bool = True) -> lo
     lg.setLevel(get_log_level())
     lg.propagate = False
     if not lg.handlers:
-        h = logging.StreamHandler(sys.stdout)
+        h = logging.StreamHandler(sys.stderr if os.environ.get("NXD_LOG_STREAM") == "stderr" else sys.stdout)
         fmt = "%(levelname)s %(name)s: %(message)s" if os.environ.get("NXD_LOG_HIDE_TIME") == "1" else \
             "%(asctime)s.%(msecs)03d %(levelname)s %(name)s: %(message)s"
         h.setFormatter(logging.Formatter(fmt, datefmt="%Y-%m-%d %H:%M:%S"))

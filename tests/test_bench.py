@@ -63,3 +63,17 @@ def test_bench_rank_failure_propagates():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in (r.stderr + r.stdout)
+
+
+def test_bench_pipeline_mode():
+    """--pp: TP = N / P x PP = P through NxDPPModel 1F1B (the BASELINE's TP=2 x PP=4 config shape)."""
+    args = ["--model", "tiny", "--seq", "128", "--gbs", "8", "--steps", "1", "--warmup", "1", "--cpu", "--pp", "2"]
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", *args], cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["config"]["parallelism"] == "tp2_sp_pp2_1f1b" and rec["config"]["grad_accum"] == 4
+    assert rec["n_gpus"] == 4 and rec["value"] > 0
+    assert abs(rec["loss"] - math.log(1024)) < 0.5, rec["loss"]
