@@ -8,6 +8,7 @@ bucketing, quantization, speculation, Medusa) plus the MI355X runtime knobs:
 * `decode_graph_steps` — decode steps captured per hipGraph replay (the whole token loop runs on
   the device: sampling, next-token feed-back and position updates are inside the graph);
 * `use_hip_graphs` — capture decode graphs at all (eager fallback for debugging).
+* `prefill_graphs` — also capture the context-encoding forward per (batch, bucket).
 """
 
 from __future__ import annotations
@@ -57,6 +58,8 @@ class InferenceConfig:
         self.temperature = kwargs.pop("temperature", 1.0)
         self.num_beams = kwargs.pop("num_beams", 1)
         self.use_hip_graphs = kwargs.pop("use_hip_graphs", True)
+        # context encoding captured per (batch, bucket) hipGraph as well (needs use_hip_graphs)
+        self.prefill_graphs = kwargs.pop("prefill_graphs", True)
         # GQA sharding (modules/gqa.py): "replicate-to-tp-degree" (default) | "convert-to-mha"
         self.gqa_sharding_strategy = kwargs.pop("gqa_sharding_strategy", None)
         # measured weight-layout pass at the context-encoding size (trace/weight_layout.py)

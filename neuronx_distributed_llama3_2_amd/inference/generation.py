@@ -67,6 +67,41 @@ def load_hf_state_dict(model_dir: str) -> Dict[str, torch.Tensor]:
     raise FileNotFoundError(f"no HF weights found in {model_dir}")
 
 
+class PrefillGraph:
+    """Context encoding of a fixed (batch, bucket) shape captured in one hipGraph: static input
+    buffers (token ids, cache rows, last-token index), positions 0..Tb-1 baked in, KV-cache writes
+    and all collectives inside the graph.  Graphs of different buckets share one memory pool (they
+    replay one at a time)."""
+
+    def __init__(self, model, B: int, Tb: int, device, pool=None):
+        self.model = model
+        self.ids = torch.zeros((B, Tb), dtype=torch.long, device=device)
+        self.seq_ids = torch.arange(B, device=device)
+        self.last = torch.full((B,), Tb - 1, dtype=torch.long, device=device)
+        self.positions = torch.arange(Tb, device=device).unsqueeze(0).expand(B, Tb).contiguous()
+        # warm-up on a side stream (GEMM autotuning, workspace allocation) before capture; it
+        # writes KV-cache rows that the real prefill overwrites
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            self._fwd()
+        torch.cuda.current_stream(device).wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        self.pool = pool if pool is not None else torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(self.graph, pool=self.pool):
+            self.out = self._fwd()
+
+    def _fwd(self):
+        return self.model.forward_tokens(self.ids, self.positions, self.seq_ids, last_index=self.last, prefill=True)
+
+    def run(self, ids: torch.Tensor, seq_ids: torch.Tensor, last_index: torch.Tensor) -> torch.Tensor:
+        self.ids.copy_(ids)
+        self.seq_ids.copy_(seq_ids)
+        self.last.copy_(last_index)
+        self.graph.replay()
+        return self.out
+
+
 class _SubModel:
     """Callable view used by benchmarks / latency collectors (reference ModelWrapper tags)."""
 
@@ -151,6 +186,8 @@ class LlamaForCausalLMInference:
         spec_slack = (K + 1) * int(getattr(config, "spec_rounds_per_graph", 4)) + 2 if K else 0
         self.cache_len = config.max_length + max(self.graph_steps, spec_slack)
         self._graphs: Dict[tuple, DecodeGraph] = {}
+        self._prefill_cache: Dict[tuple, "PrefillGraph"] = {}
+        self._prefill_pool = None
         self._states: Dict[int, DecodeState] = {}
         self.kv_cache_populated = False
         self.context_encoding_model = _SubModel(self, CONTEXT_ENCODING_MODEL)
@@ -216,6 +253,9 @@ class LlamaForCausalLMInference:
             self.weight_layouts = optimize_weight_layout(self.model, int(self.config.max_context_length) * self.max_batch,
                                                          path=getattr(self, "_layout_dir", None))
         self.model.setup_kv_cache(self.max_batch, self.cache_len, self.device)
+        # captured graphs hold the previous weight / cache tensors
+        self._graphs.clear()
+        self._prefill_cache.clear()
 
     def compile(self, serialize_base_path: str) -> None:
         """Write this rank's weight shard + configs (the reference's trace/compile step; there is
@@ -268,11 +308,28 @@ class LlamaForCausalLMInference:
         pad = self.model_config.pad_token_id if getattr(self.model_config, "pad_token_id", None) is not None else 0
         ids, mask = pad_to_bucket(input_ids, attention_mask, self.config.buckets + [self.config.max_length], pad)
         Tb = ids.shape[1]
-        positions = torch.arange(Tb, device=dev).unsqueeze(0).expand(B, Tb)
         seq_ids = torch.arange(B, device=dev) if seq_ids is None else seq_ids.to(dev)
-        logits = self.model.forward_tokens(ids, positions, seq_ids, last_index=lengths - 1, prefill=True)
+        if self._prefill_graphs_on():
+            logits = self._prefill_graph(B, Tb).run(ids, seq_ids, lengths - 1)
+        else:
+            positions = torch.arange(Tb, device=dev).unsqueeze(0).expand(B, Tb)
+            logits = self.model.forward_tokens(ids, positions, seq_ids, last_index=lengths - 1, prefill=True)
         self.kv_cache_populated = True
         return logits.float()
+
+    def _prefill_graphs_on(self) -> bool:
+        return (self.device.type == "cuda" and getattr(self.config, "prefill_graphs", True)
+                and getattr(self.config, "use_hip_graphs", True))
+
+    def _prefill_graph(self, B: int, Tb: int) -> "PrefillGraph":
+        """One captured context-encoding forward per (batch, bucket) -- the reference compiles one
+        NEFF per bucket; here a hipGraph per bucket removes the per-kernel launch cost of prefill."""
+        key = (B, Tb)
+        g = self._prefill_cache.get(key)
+        if g is None:
+            g = self._prefill_cache[key] = PrefillGraph(self.model, B, Tb, self.device, self._prefill_pool)
+            self._prefill_pool = g.pool
+        return g
 
     def _token_generate(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                         position_ids: Optional[torch.Tensor] = None, seq_ids: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -238,3 +238,32 @@ def test_weight_layout_pass_on_gpu(hf_sd):
         out = m._context_encode(ids).cpu()
         err = (out - ref).abs().max() / ref.abs().max()
         assert err < 1e-2, err
+
+
+def test_prefill_graphs_match_eager(hf_sd):
+    """Context encoding replayed from per-(batch, bucket) hipGraphs == the eager forward, across
+    buckets and repeated calls; greedy generation after a graphed prefill is unchanged."""
+    from neuronx_distributed_llama3_2_amd.inference import InferenceConfig, LlamaForCausalLMInference
+    from neuronx_distributed_llama3_2_amd.models.llama.convert import hf_to_nxd
+
+    cfg, sd = hf_sd
+    models = {}
+    for graphs in (True, False):
+        icfg = InferenceConfig(batch_size=2, seq_len=256, max_context_length=128, prefill_graphs=graphs)
+        m = LlamaForCausalLMInference(cfg, icfg, dtype=torch.bfloat16, device=torch.device("cuda"), init_weights=False)
+        m._load_full(hf_to_nxd(sd, cfg))
+        models[graphs] = m
+    torch.manual_seed(5)
+    for T in (100, 30, 100):
+        ids = torch.randint(3, cfg.vocab_size, (2, T))
+        mask = torch.ones_like(ids)
+        mask[1, T // 2:] = 0
+        a = models[True]._context_encode(ids, mask)
+        b = models[False]._context_encode(ids, mask)
+        assert (a - b).abs().max().item() <= 1e-2 * b.abs().max().item()
+    assert len(models[True]._prefill_cache) == 1 and not models[False]._prefill_cache  # one (2, 128) bucket
+    ids = torch.randint(3, cfg.vocab_size, (1, 40))
+    ga = models[True].generate(ids, max_new_tokens=12, eos_token_id=-1)
+    gb = models[False].generate(ids, max_new_tokens=12, eos_token_id=-1)
+    assert torch.equal(ga, gb)
+    assert len(models[True]._prefill_cache) == 2   # + (1, 128)
