@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--quantized", default=None, choices=[None, "per_tensor_symmetric", "per_channel_symmetric"])
     ap.add_argument("--report", default="gpurun_out/benchmark_report.json")
+    ap.add_argument("--weight-layout", action="store_true",
+                    help="measured weight-layout pass at the prompt size (trace/weight_layout.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -50,6 +52,11 @@ def main():
                            quantization_type=args.quantized or "per_tensor_symmetric")
     torch.manual_seed(0)
     model = LlamaForCausalLMInference(mcfg, icfg, dtype=torch.bfloat16)
+    layouts = None
+    if args.weight_layout:
+        from neuronx_distributed_llama3_2_amd.trace.weight_layout import optimize_weight_layout
+
+        layouts = optimize_weight_layout(model.model, args.prompt * args.batch)
     g = torch.Generator().manual_seed(1)
     ids = torch.randint(10, mcfg.vocab_size, (args.batch, args.prompt), generator=g)
     mask = torch.ones_like(ids)
@@ -73,6 +80,8 @@ def main():
     report["config"] = {"model": args.model, "tp": world, "batch": args.batch, "prompt": args.prompt,
                         "new_tokens": args.new, "dtype": "bf16", "graph_steps": args.graph_steps,
                         "hip_graphs": not args.no_graphs, "quantized": args.quantized,
+                        "weight_layouts": None if layouts is None else {v: sum(1 for x in layouts.values() if x == v)
+                                                                        for v in set(layouts.values())},
                         "data": "synthetic prompt, random-init weights"}
     if not dist.is_initialized() or dist.get_rank() == 0:
         os.makedirs(os.path.dirname(args.report) or ".", exist_ok=True)
