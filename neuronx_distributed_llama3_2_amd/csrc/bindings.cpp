@@ -40,6 +40,8 @@ int decode_attn_launch(const void*, const int64_t*, const void*, const void*, co
 int kv_cache_write_launch(const void*, const void*, const int64_t*, void*, void*, const int64_t*, const int*, const int*,
                           int, int, int, int, int, hipStream_t);
 int argmax_launch(const void*, int, int64_t, int, int, int64_t*, hipStream_t);
+int greedy_advance_launch(const void*, int, int64_t, int, int, unsigned long long*, int64_t*, int64_t, int, int64_t*, int64_t*,
+                          int64_t*, int*, hipStream_t);
 int topk_sample_launch(const void*, int, int64_t, int, int, int, float, const float*, int64_t*, float*, int64_t*,
                        hipStream_t);
 int gemv_launch(const void*, int64_t, const void*, int64_t, int, const float*, float, const void*, void*, int64_t, int, int,
@@ -464,6 +466,29 @@ void argmax_rows(at::Tensor x, at::Tensor out) {
            "argmax");
 }
 
+// greedy decode tail: argmax of logits [B, V] -> out[:, step], tokens, positions + 1, cache_len + 1,
+// step + 1 (the decode loop's feed-back, graph-capturable); slot: int64 [B] zeros between calls
+void greedy_advance(at::Tensor logits, at::Tensor slot, at::Tensor out, at::Tensor step, at::Tensor tokens,
+                    at::Tensor positions, at::Tensor cache_len) {
+  check_cuda(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [B, V] with unit stride");
+  TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16, "logits must be fp32/bf16");
+  const int64_t B = logits.size(0);
+  TORCH_CHECK(slot.scalar_type() == at::kLong && slot.numel() == B && slot.is_contiguous(), "slot: int64 [B]");
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.dim() == 2 && out.size(0) == B && out.stride(1) == 1, "out: int64 [B, S]");
+  TORCH_CHECK(step.scalar_type() == at::kLong && step.numel() == 1, "step: int64 [1]");
+  TORCH_CHECK(tokens.scalar_type() == at::kLong && tokens.numel() == B && tokens.is_contiguous(), "tokens: int64 [B]");
+  TORCH_CHECK(positions.scalar_type() == at::kLong && positions.numel() == B && positions.is_contiguous(), "positions: int64 [B]");
+  TORCH_CHECK(cache_len.scalar_type() == at::kInt && cache_len.numel() == B && cache_len.is_contiguous(), "cache_len: int32 [B]");
+  for (const at::Tensor* t : {&slot, &out, &step, &tokens, &positions, &cache_len}) check_cuda(*t, "decode state");
+  check_rc(nxd::greedy_advance_launch(logits.data_ptr(), logits.scalar_type() == at::kFloat, logits.stride(0), (int)B,
+                                      (int)logits.size(1), reinterpret_cast<unsigned long long*>(slot.data_ptr<int64_t>()),
+                                      out.data_ptr<int64_t>(), out.stride(0), (int)out.size(1), step.data_ptr<int64_t>(),
+                                      tokens.data_ptr<int64_t>(), positions.data_ptr<int64_t>(), cache_len.data_ptr<int>(),
+                                      cur_stream()),
+           "greedy_advance");
+}
+
 void topk_sample(at::Tensor x, int64_t k, double temperature, c10::optional<at::Tensor> uniform, at::Tensor out,
                  c10::optional<at::Tensor> vals, c10::optional<at::Tensor> idx) {
   check_cuda(x, "x");
@@ -728,6 +753,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_attn", &decode_attn);
   m.def("kv_cache_write", &kv_cache_write);
   m.def("argmax_rows", &argmax_rows);
+  m.def("greedy_advance", &greedy_advance);
   m.def("topk_sample", &topk_sample);
   m.attr("ARCH") = "gfx950";
 }

@@ -368,6 +368,70 @@ __device__ __forceinline__ uint32_t fkey(float f) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// ---- greedy decode step tail: argmax over the vocabulary split across many workgroups (one
+// 64-bit atomicMax of (order-preserving value key, ~index) per workgroup: highest logit, lowest
+// index on ties, as torch.argmax), then ONE tiny kernel that feeds the token back: out[b, step],
+// tokens[b], positions[b] + 1, cache_len[b] + 1, step + 1 and the slot reset -- instead of the
+// single-workgroup argmax plus five framework element-wise launches per token.
+constexpr int kArgmaxChunk = 2048;   // elements per workgroup (256 threads x 8)
+
+template <typename T>
+__global__ void __launch_bounds__(256) argmax_partial_kernel(const T* __restrict__ x, int64_t ld, int V,
+                                                             unsigned long long* __restrict__ slot) {
+  __shared__ unsigned long long wk[4];
+  const int b = blockIdx.y;
+  const T* row = x + (int64_t)b * ld;
+  const int beg = blockIdx.x * kArgmaxChunk, end = min(V, beg + kArgmaxChunk);
+  float best = -INFINITY;
+  int idx = -1;
+  const int i0 = beg + threadIdx.x * 8;
+  if (sizeof(T) == 2 && (reinterpret_cast<uintptr_t>(row) % 16) == 0 && i0 + 8 <= end) {
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4_t*>(row + i0), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (f[e] > best) { best = f[e]; idx = i0 + e; }
+  } else {
+    for (int i = i0; i < min(end, i0 + 8); ++i) {
+      const float v = ldv<T>(row, i);
+      if (idx < 0 || v > best) { best = v; idx = i; }
+    }
+  }
+  unsigned long long key = idx < 0 ? 0ull
+                                   : ((unsigned long long)fkey(best) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)idx);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long ok = __shfl_xor(key, o, 64);
+    key = ok > key ? ok : key;
+  }
+  if ((threadIdx.x & 63) == 0) wk[threadIdx.x >> 6] = key;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long k = wk[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) k = wk[w] > k ? wk[w] : k;
+    if (k) atomicMax(slot + b, k);
+  }
+}
+
+__global__ void __launch_bounds__(64) greedy_advance_kernel(unsigned long long* __restrict__ slot, int64_t* __restrict__ out,
+                                                           int64_t ld_out, int max_steps, int64_t* __restrict__ step,
+                                                           int64_t* __restrict__ tokens, int64_t* __restrict__ positions,
+                                                           int* __restrict__ cache_len, int B) {
+  const int64_t s = step[0];
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const unsigned long long k = slot[b];
+    const int64_t tok = k ? (int64_t)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : 0;
+    if (s >= 0 && s < max_steps) out[(int64_t)b * ld_out + s] = tok;
+    tokens[b] = tok;
+    positions[b] += 1;
+    cache_len[b] += 1;
+    slot[b] = 0ull;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) step[0] = s + 1;
+}
+
 constexpr int kMaxTopK = 1024;
 
 template <typename T>
@@ -544,6 +608,21 @@ int topk_sample_launch(const void* x, int is_fp32, int64_t ld, int B, int V, int
     hipLaunchKernelGGL(dec::topk_sample_kernel<float>, dim3(B), dim3(1024), 0, stream, (const float*)x, ld, V, K, inv_t, uniform, out, out_vals, out_idx);
   else
     hipLaunchKernelGGL(dec::topk_sample_kernel<uint16_t>, dim3(B), dim3(1024), 0, stream, (const uint16_t*)x, ld, V, K, inv_t, uniform, out, out_vals, out_idx);
+  return (int)hipGetLastError();
+}
+
+int greedy_advance_launch(const void* logits, int is_fp32, int64_t ld, int B, int V, unsigned long long* slot, int64_t* out,
+                          int64_t ld_out, int max_steps, int64_t* step, int64_t* tokens, int64_t* positions, int* cache_len,
+                          hipStream_t stream) {
+  if (B == 0) return 0;
+  if (B > 65535) return -1;
+  const dim3 grid((unsigned)((V + dec::kArgmaxChunk - 1) / dec::kArgmaxChunk), (unsigned)B);
+  if (is_fp32)
+    hipLaunchKernelGGL(dec::argmax_partial_kernel<float>, grid, dim3(256), 0, stream, (const float*)logits, ld, V, slot);
+  else
+    hipLaunchKernelGGL(dec::argmax_partial_kernel<uint16_t>, grid, dim3(256), 0, stream, (const uint16_t*)logits, ld, V, slot);
+  hipLaunchKernelGGL(dec::greedy_advance_kernel, dim3(1), dim3(64), 0, stream, slot, out, ld_out, max_steps, step, tokens,
+                     positions, cache_len, B);
   return (int)hipGetLastError();
 }
 

@@ -76,7 +76,7 @@ class PrefillGraph:
     def __init__(self, model, B: int, Tb: int, device, pool=None):
         self.model = model
         self.ids = torch.zeros((B, Tb), dtype=torch.long, device=device)
-        self.seq_ids = torch.arange(B, device=device)
+        self.seq_ids = torch.arange(B, dtype=torch.int32, device=device)
         self.last = torch.full((B,), Tb - 1, dtype=torch.long, device=device)
         self.positions = torch.arange(Tb, device=device).unsqueeze(0).expand(B, Tb).contiguous()
         # warm-up on a side stream (GEMM autotuning, workspace allocation) before capture; it

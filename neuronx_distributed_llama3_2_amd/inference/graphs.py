@@ -11,11 +11,16 @@ with ONE host launch and no synchronisation.  The host only checks for EOS betwe
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
 
+from .. import ops
 from ..utils.sampling import Sampler
+
+# greedy decoding ends each step with the fused argmax + feed-back launch pair (ops.greedy_advance_)
+GREEDY_FUSED = os.environ.get("NXD_GREEDY_FUSED", "1") == "1"
 
 
 class DecodeState:
@@ -25,10 +30,12 @@ class DecodeState:
         self.tokens = torch.zeros((batch, 1), dtype=torch.int64, device=device)
         self.positions = torch.zeros((batch, 1), dtype=torch.int64, device=device)
         self.cache_len = torch.ones(batch, dtype=torch.int32, device=device)
-        self.seq_ids = torch.arange(batch, dtype=torch.int64, device=device)
+        # int32: the cache-row index the decode kernels take (no per-step conversion launch)
+        self.seq_ids = torch.arange(batch, dtype=torch.int32, device=device)
         self.out = torch.zeros((batch, max_steps), dtype=torch.int64, device=device)
         self.step = torch.zeros(1, dtype=torch.int64, device=device)
         self.uniform = torch.rand((max_steps, batch), dtype=torch.float32, device=device)
+        self.argmax_slot = torch.zeros(batch, dtype=torch.int64, device=device)
         self.batch, self.max_steps = batch, max_steps
 
     def load(self, first_tokens: torch.Tensor, start_positions: torch.Tensor, seq_ids: Optional[torch.Tensor] = None,
@@ -50,6 +57,9 @@ def decode_step(model, sampler: Sampler, st: DecodeState) -> None:
     """One token for every sequence; all state lives in `st` (graph-capturable)."""
     B = st.batch
     logits = model.forward_tokens(st.tokens, st.positions, st.seq_ids, st.cache_len)[:, -1]
+    if GREEDY_FUSED and sampler.top_k == 1 and not getattr(sampler, "is_medusa", False):
+        ops.greedy_advance_(logits, st.argmax_slot, st.out, st.step, st.tokens, st.positions, st.cache_len)
+        return
     u = st.uniform.index_select(0, st.step).view(B)
     nxt = sampler.sample(logits, u)
     st.out.scatter_(1, st.step.view(1, 1).expand(B, 1), nxt.view(B, 1))

@@ -73,6 +73,24 @@ def argmax_rows(x: torch.Tensor) -> torch.Tensor:
     return torch.argmax(x, dim=-1)
 
 
+def greedy_advance_(logits: torch.Tensor, slot: torch.Tensor, out: torch.Tensor, step: torch.Tensor,
+                    tokens: torch.Tensor, positions: torch.Tensor, cache_len: torch.Tensor) -> None:
+    """Greedy decode tail in two launches (multi-workgroup argmax + state feed-back):
+    t = argmax(logits, -1); out[:, step] = t; tokens = t; positions += 1; cache_len += 1; step += 1.
+    `slot` is int64 [B] scratch that must be zero on entry (the kernel leaves it zeroed)."""
+    if use_native(logits):
+        ext().greedy_advance(logits if logits.stride(-1) == 1 else logits.contiguous(), slot, out, step,
+                             tokens.view(-1), positions.view(-1), cache_len.view(-1))
+        return
+    t = torch.argmax(logits, dim=-1)
+    B = logits.shape[0]
+    out.scatter_(1, step.view(1, 1).expand(B, 1), t.view(B, 1))
+    tokens.copy_(t.view(tokens.shape))
+    positions.add_(1)
+    cache_len.add_(1)
+    step.add_(1)
+
+
 def topk_sample(x: torch.Tensor, top_k: int, temperature: float = 1.0, uniform: Optional[torch.Tensor] = None,
                 return_topk: bool = False):
     """Multinomial sampling among the top-k logits (reference Sampler.multinomial semantics:

@@ -267,3 +267,45 @@ def test_prefill_graphs_match_eager(hf_sd):
     gb = models[False].generate(ids, max_new_tokens=12, eos_token_id=-1)
     assert torch.equal(ga, gb)
     assert len(models[True]._prefill_cache) == 2   # + (1, 128)
+
+
+@pytest.mark.parametrize("V,dtype", [(128256, torch.bfloat16), (1001, torch.bfloat16), (5000, torch.float32)])
+def test_greedy_advance_kernel(V, dtype):
+    """Multi-workgroup argmax (ties -> lowest index, as torch.argmax) + decode-state feed-back."""
+    from neuronx_distributed_llama3_2_amd import ops
+
+    torch.manual_seed(V)
+    B, S = 3, 8
+    logits = torch.randn(B, V, device="cuda").to(dtype)
+    logits[1, V // 3] = logits[1, V - 1] = 50.0          # tie: the first one wins
+    logits[2] = -1.0                                      # all equal: index 0
+    slot = torch.zeros(B, dtype=torch.int64, device="cuda")
+    out = torch.zeros(B, S, dtype=torch.int64, device="cuda")
+    step = torch.tensor([2], dtype=torch.int64, device="cuda")
+    tokens = torch.zeros(B, 1, dtype=torch.int64, device="cuda")
+    positions = torch.tensor([[5], [6], [7]], device="cuda")
+    cache_len = torch.tensor([6, 7, 8], dtype=torch.int32, device="cuda")
+    ops.greedy_advance_(logits, slot, out, step, tokens, positions, cache_len)
+    ref = torch.argmax(logits.float(), dim=-1)
+    assert torch.equal(tokens.view(-1), ref) and int(ref[1]) == V // 3 and int(ref[2]) == 0
+    assert torch.equal(out[:, 2], ref) and int(out[:, [0, 1, 3]].abs().sum()) == 0
+    assert int(step) == 3 and positions.view(-1).tolist() == [6, 7, 8] and cache_len.tolist() == [7, 8, 9]
+    assert int(slot.abs().sum()) == 0
+
+
+def test_greedy_fused_decode_matches_unfused(hf_sd):
+    from neuronx_distributed_llama3_2_amd.inference import graphs
+
+    cfg, sd = hf_sd
+    m = _model(cfg, sd, torch.bfloat16, device=torch.device("cuda"))
+    torch.manual_seed(9)
+    ids = torch.randint(3, cfg.vocab_size, (2, 33))
+    outs = []
+    for fused in (True, False):
+        graphs.GREEDY_FUSED = fused
+        m._graphs.clear()
+        try:
+            outs.append(m.generate(ids, max_new_tokens=20, eos_token_id=-1))
+        finally:
+            graphs.GREEDY_FUSED = True
+    assert torch.equal(outs[0], outs[1])
