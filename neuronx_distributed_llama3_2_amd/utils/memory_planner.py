@@ -13,15 +13,18 @@ so this module answers it from measured coefficients of THIS framework's trainin
   (profiles/r2_activation_memory.jsonl): Llama-3-8B TP=1 34.0 h without recompute (flash
   attention keeps no S x S matrix, so "selective" recompute saves nothing) and 4.0 h with full
   recompute; Llama-3-70B at TP=8 per-rank shapes 11.2 h, which splits the 34 h into 7.9 h of
-  hidden-sized tensors (norm inputs / outputs, residuals: divided by TP only under sequence
-  parallelism) and 26.1 h of tensor-parallel tensors (QKV, attention output, gate/up, SwiGLU:
-  divided by TP);
+  hidden-sized tensors and 26.1 h of tensor-parallel tensors (QKV, attention output, gate/up,
+  SwiGLU: divided by TP).  Of the hidden-sized 7.9 h, the two normalised inputs of the
+  column-parallel projections (4 h) are kept all-gathered under sequence parallelism when the
+  layers save the gathered input for the weight gradient (parallel_layers/layers.py, the default:
+  no re-gather in backward), the rest (3.9 h: residuals, norm inputs) is divided by TP;
 * fixed activation bytes: logits + loss, 2.5 bytes per (token, local vocab entry) measured.
 
 Calibration check: Llama-3-8B TP=1 mbs 1 plans to 186 GiB against the 189.0 GiB peak bench.py
 measures (profiles/r2_bench_1gpu_v4.log).  Llama-3-70B at TP=8 with sequence parallelism plans to
-186 / 207 / 229 GiB at 1 / 2 / 3 sequences per micro-batch: it trains on ONE 8-GPU node without
-pipeline stages and without activation recompute (the reference runs it at TP=32 x PP=8).
+203 GiB at 1 sequence per micro-batch (187 GiB without the saved gathered inputs): it trains on ONE
+8-GPU node without pipeline stages and without activation recompute (the reference runs it at
+TP=32 x PP=8).
 """
 
 from __future__ import annotations
@@ -33,10 +36,10 @@ from typing import Optional
 HBM_BYTES_MI355X = 288 * 10**9
 
 RESIDENT_BYTES_PER_PARAM = {"weight": 2.0, "dgrad_kmajor": 2.0, "main_grad": 4.0, "master": 4.0, "adam_moments": 8.0}
-ACT_COEF = {
-    "none": {"replicated": 7.9, "tp_split": 26.1},   # x h bytes per token per layer
-    "selective": {"replicated": 7.9, "tp_split": 26.1},
-    "full": {"replicated": 4.0, "tp_split": 0.0},
+ACT_COEF = {   # x h bytes per token per layer
+    "none": {"sp_split": 3.9, "gathered": 4.0, "tp_split": 26.1},
+    "selective": {"sp_split": 3.9, "gathered": 4.0, "tp_split": 26.1},
+    "full": {"sp_split": 4.0, "gathered": 0.0, "tp_split": 0.0},
 }
 LOGIT_BYTES = 2.5  # per (token, local vocab entry): bf16 logits + fp32 loss workspace
 GIB = 2**30
@@ -101,7 +104,7 @@ def params_per_rank(cfg, tp: int = 1, pp: int = 1, stage: Optional[int] = None) 
 
 def plan_training_memory(cfg, tp: int = 1, pp: int = 1, dp: int = 1, mbs: int = 1, seq: int = 8192,
                          sequence_parallel: Optional[bool] = None, activation_checkpoint: Optional[str] = None,
-                         zero1: bool = True, num_microbatches: int = 1,
+                         zero1: bool = True, num_microbatches: int = 1, save_gathered_input: bool = True,
                          hbm_bytes: float = HBM_BYTES_MI355X) -> MemoryPlan:
     """Peak bytes of one rank of a TP x PP x DP training job (fp32-master AdamW, bf16 compute)."""
     if sequence_parallel is None:
@@ -117,7 +120,9 @@ def plan_training_memory(cfg, tp: int = 1, pp: int = 1, dp: int = 1, mbs: int = 
     shard = dp if zero1 else 1
     resident = n * (r["weight"] + r["dgrad_kmajor"] + r["main_grad"] + (r["master"] + r["adam_moments"]) / shard)
     coef = ACT_COEF[mode]
-    per_token_layer = h * (coef["replicated"] / (tp if sequence_parallel else 1) + coef["tp_split"] / tp)
+    sp_div = tp if sequence_parallel else 1
+    gathered_div = 1 if (save_gathered_input or not sequence_parallel) else tp
+    per_token_layer = h * (coef["sp_split"] / sp_div + coef["gathered"] / gathered_div + coef["tp_split"] / tp)
     lps = math.ceil(L / pp)
     # 1F1B: the first stage holds the activations of up to `pp` micro-batches at once
     in_flight = min(pp, max(1, num_microbatches)) if pp > 1 else 1

@@ -36,6 +36,8 @@ def test_llama3_70b_tp8_fits_one_node():
     assert plan_training_memory(c70, tp=8, activation_checkpoint="full").activation_bytes < p1.activation_bytes
     assert plan_training_memory(c70, tp=8, dp=4).resident_bytes < p1.resident_bytes
     assert largest_micro_batch(c70, tp=8) >= 2
+    # re-gathering the column-parallel inputs in backward (instead of saving them) trades comm for memory
+    assert plan_training_memory(c70, tp=8, save_gathered_input=False).total_bytes < p1.total_bytes
     assert not plan_training_memory(c70, tp=1).fits   # 70B needs model parallelism
     with pytest.raises(ValueError):
         plan_training_memory(c70, activation_checkpoint="bogus")
