@@ -29,7 +29,7 @@ def test_plan_matches_measured_bench_peak():
 def test_llama3_70b_tp8_fits_one_node():
     c70 = llama_config("llama3-70b")
     p1 = plan_training_memory(c70, tp=8, mbs=1)
-    assert p1.fits and p1.total_bytes / GIB < 200
+    assert p1.fits and p1.total_bytes / GIB < 210
     # sequence parallelism divides the hidden-sized activations by TP
     assert plan_training_memory(c70, tp=8, sequence_parallel=False).total_bytes > p1.total_bytes
     # full recompute shrinks activations; ZeRO-1 over DP shrinks the optimizer state
