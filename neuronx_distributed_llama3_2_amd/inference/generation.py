@@ -323,7 +323,8 @@ class LlamaForCausalLMInference:
 
     def _prefill_graph(self, B: int, Tb: int) -> "PrefillGraph":
         """One captured context-encoding forward per (batch, bucket) -- the reference compiles one
-        NEFF per bucket; here a hipGraph per bucket removes the per-kernel launch cost of prefill."""
+        NEFF per bucket (trace/model_builder.py:380-451, SPMDBucketModel trace/spmd.py:32-61); here a
+        hipGraph per bucket removes the per-kernel launch cost of prefill."""
         key = (B, Tb)
         g = self._prefill_cache.get(key)
         if g is None:
