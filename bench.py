@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--no-sp", action="store_true")
     ap.add_argument("--ckpt", default=None, help="activation checkpointing: None | full | selective")
     ap.add_argument("--cpu", action="store_true", help="force the CPU/gloo path (plumbing tests)")
+    ap.add_argument("--gloo-gpu", action="store_true",
+                    help="test mode: every rank on cuda:0 with gloo collectives on staged GPU tensors (multi-rank "
+                         "rehearsal of the GPU code path on a one-GPU box; not a measurement)")
     return ap.parse_args()
 
 
@@ -141,6 +144,8 @@ def main(a):
     if world != a.gpus:
         raise SystemExit(f"bench: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
     use_cuda = torch.cuda.is_available() and not a.cpu
+    if use_cuda and a.gloo_gpu:
+        local_rank = 0
     if use_cuda:
         ndev = torch.cuda.device_count()
         if local_rank >= ndev:
@@ -150,12 +155,12 @@ def main(a):
     os.environ.setdefault("MASTER_PORT", "29511")
     if not use_cuda:
         torch.set_num_threads(max(1, (os.cpu_count() or 1) // world))
-    backend = "nccl" if use_cuda else "gloo"
+    backend = "nccl" if use_cuda and not a.gloo_gpu else "gloo"
     from neuronx_distributed_llama3_2_amd.parallel.rccl_env import apply_rccl_env
 
     apply_rccl_env()
     dist.init_process_group(backend, rank=rank, world_size=world,
-                            device_id=torch.device("cuda", local_rank) if use_cuda else None)
+                            device_id=torch.device("cuda", local_rank) if use_cuda and backend == "nccl" else None)
     dev = torch.device("cuda", local_rank) if use_cuda else torch.device("cpu")
     # preflight: one all-reduce over the whole job must see every rank (RCCL on GPU)
     probe = torch.ones(1, device=dev)

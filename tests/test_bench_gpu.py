@@ -1,0 +1,42 @@
+"""bench.py's multi-rank GPU code path rehearsed on the one-GPU test box: N ranks share cuda:0 with
+gloo collectives on staged GPU tensors (bench.py --gloo-gpu).  Everything but RCCL runs as in the
+driver's 2/4/8-GPU bench: the HIP kernels at TP shapes with sequence parallelism, the flat
+grad buffers and fused AdamW (ZeRO-1 over DP), the timing/JSON contract."""
+
+import json
+import math
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(n, *extra):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    args = ["--model", "tiny", "--seq", "512", "--gbs", "8", "--steps", "2", "--warmup", "1", "--gloo-gpu", *extra]
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), *args], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(recs) == 1, r.stdout
+    return recs[0]
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_tp_sp_ranks_on_one_gpu(n):
+    rec = _run(n)
+    assert rec["config"]["parallelism"] == f"tp{n}_sp" and rec["n_gpus"] == n and rec["comm_world_size"] == n
+    assert rec["value"] > 0 and abs(rec["loss"] - math.log(1024)) < 0.5, rec
+
+
+def test_bench_dp_zero1_ranks_on_one_gpu():
+    rec = _run(2, "--parallelism", "dp")
+    assert rec["config"]["parallelism"] == "tp1_dp2_zero1" and rec["value"] > 0
+    assert abs(rec["loss"] - math.log(1024)) < 0.5, rec
