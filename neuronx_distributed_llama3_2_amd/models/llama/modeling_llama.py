@@ -248,6 +248,11 @@ def llama_config(name: str = "llama3-8b", **overrides):
         "tiny": dict(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
                      num_key_value_heads=2, vocab_size=1024, rope_theta=10000.0, max_position_embeddings=512,
                      rms_norm_eps=1e-5),
+        # Llama-3-8B's head geometry scaled down (32 / 8 heads of 128 -> 16 / 8 of 64): TP = 8 keeps one
+        # KV head per rank as the headline config does (multi-rank rehearsals, tests)
+        "tiny8": dict(hidden_size=1024, intermediate_size=2048, num_hidden_layers=2, num_attention_heads=16,
+                      num_key_value_heads=8, vocab_size=1024, rope_theta=10000.0, max_position_embeddings=512,
+                      rms_norm_eps=1e-5),
     }
     kw = dict(presets[name])
     kw.setdefault("initializer_range", 0.02)
