@@ -55,6 +55,9 @@ int dgemv_launch(int, const void*, int64_t, const void*, float, const void*, int
                  int, int, const float*, const float*, const int64_t*, int, void*, void*, int64_t, int64_t, int64_t,
                  const int*, int, int, hipStream_t);
 int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, int, hipStream_t);
+int moe_combine_fwd_launch(const void*, const int64_t*, const float*, void*, int64_t, int, int, hipStream_t);
+int moe_combine_bwd_launch(const void*, const void*, const int64_t*, const float*, void*, float*, int64_t, int, int,
+                           hipStream_t);
 }  // namespace nxd
 
 namespace {
@@ -636,6 +639,51 @@ void grouped_gemm(int64_t mode, at::Tensor a, at::Tensor b, at::Tensor offs, at:
            "grouped_gemm");
 }
 
+// MoE un-permute + affinity-weighted combine (csrc/moe_combine.hip).  ys [T*k, H] bf16 in
+// expert-sorted order, inv int64 [T*k], aff fp32 [T, k] (undefined tensor: unit weights), out [T, H].
+void moe_combine_check(const at::Tensor& ys, const at::Tensor& inv, const at::Tensor& aff, int64_t T, int64_t k) {
+  check_bf16(ys, "ys");
+  check_cuda(inv, "inv");
+  TORCH_CHECK(ys.dim() == 2 && ys.is_contiguous() && ys.size(0) == T * k, "moe_combine: ys must be contiguous [T*k, H]");
+  TORCH_CHECK(ys.size(1) % 8 == 0 && ys.size(1) < (1LL << 31), "moe_combine: H must be a multiple of 8");
+  TORCH_CHECK(inv.scalar_type() == at::kLong && inv.is_contiguous() && inv.numel() == T * k, "moe_combine: inv int64 [T*k]");
+  TORCH_CHECK(k >= 1 && k <= 8, "moe_combine: top_k must be in [1, 8]");
+  if (aff.defined()) {
+    check_cuda(aff, "aff");
+    TORCH_CHECK(aff.scalar_type() == at::kFloat && aff.is_contiguous() && aff.numel() == T * k, "moe_combine: aff fp32 [T, k]");
+  }
+  check_aligned16(ys, "ys");
+}
+
+void moe_combine_fwd(at::Tensor ys, at::Tensor inv, c10::optional<at::Tensor> aff, at::Tensor out) {
+  const int64_t T = out.size(0), H = ys.size(1), k = T ? ys.size(0) / T : 1;
+  const at::Tensor a = aff.has_value() ? *aff : at::Tensor();
+  moe_combine_check(ys, inv, a, T, k);
+  check_bf16(out, "out");
+  TORCH_CHECK(out.dim() == 2 && out.is_contiguous() && out.size(1) == H, "moe_combine: out must be contiguous [T, H]");
+  check_aligned16(out, "out");
+  check_rc(nxd::moe_combine_fwd_launch(ys.data_ptr(), inv.data_ptr<int64_t>(), a.defined() ? a.data_ptr<float>() : nullptr,
+                                       out.data_ptr(), T, (int)k, (int)H, cur_stream()),
+           "moe_combine_fwd");
+}
+
+void moe_combine_bwd(at::Tensor dout, at::Tensor ys, at::Tensor inv, at::Tensor aff, at::Tensor dys, at::Tensor daff) {
+  const int64_t T = dout.size(0), H = ys.size(1), k = T ? ys.size(0) / T : 1;
+  TORCH_CHECK(aff.defined(), "moe_combine_bwd: affinities required");
+  moe_combine_check(ys, inv, aff, T, k);
+  check_bf16(dout, "dout");
+  check_bf16(dys, "dys");
+  TORCH_CHECK(dout.dim() == 2 && dout.is_contiguous() && dout.size(1) == H, "moe_combine_bwd: dout [T, H]");
+  TORCH_CHECK(dys.sizes() == ys.sizes() && dys.is_contiguous(), "moe_combine_bwd: dys like ys");
+  TORCH_CHECK(daff.scalar_type() == at::kFloat && daff.is_contiguous() && daff.numel() == T * k && daff.is_cuda(),
+              "moe_combine_bwd: daff fp32 [T, k]");
+  check_aligned16(dout, "dout");
+  check_aligned16(dys, "dys");
+  check_rc(nxd::moe_combine_bwd_launch(dout.data_ptr(), ys.data_ptr(), inv.data_ptr<int64_t>(), aff.data_ptr<float>(),
+                                       dys.data_ptr(), daff.data_ptr<float>(), T, (int)k, (int)H, cur_stream()),
+           "moe_combine_bwd");
+}
+
 // Fused decode GEMV (csrc/decode_fused.hip).  epi: 0 plain, 1 residual add into y (in place),
 // 2 SwiGLU on a fused [2N, K] gate/up weight, 3 QKV with RoPE + KV-cache write.  norm_w: RMSNorm
 // of x fused as a prologue.  x [M, K], w [Nw, K], y [M, N] bf16, M <= 8.
@@ -722,6 +770,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("dequant_int8", &dequant_int8);
   m.def("expert_gemv", &expert_gemv);
   m.def("grouped_gemm", &grouped_gemm);
+  m.def("moe_combine_fwd", &moe_combine_fwd);
+  m.def("moe_combine_bwd", &moe_combine_bwd);
   m.def("dgemv", &dgemv);
   // decode A/B knobs: 0 = GLU row pairs per wave, 1 = GEMV k-slices (0 auto), 2 = MFMA decode attention on/off
   m.def("decode_set_knob", [](int which, int value) {

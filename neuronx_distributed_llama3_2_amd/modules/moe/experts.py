@@ -136,14 +136,16 @@ class ExpertMLPs(nn.Module):
         # device-side permutation: stable sort of the T*k slots by expert, group offsets by a
         # cumsum of the per-expert counts -- no group size ever reaches the host
         order, inverse, offs = ops.moe_permutation(expert_index, self.num_experts)
-        x_sorted = hidden_states.index_select(0, order // k)
+        x_sorted = ops.moe_dispatch(hidden_states, order, inverse, k)
         w_gu, w_d = self.mlp_op.gate_up_proj.weight, self.mlp_op.down_proj.weight
-        h = self.mlp_op._activation(ops.grouped_linear(x_sorted, w_gu, offs))
-        y_sorted = ops.grouped_linear(h, w_d, offs)            # [T*k, H] TP-partial
-        # un-permute by gathering each (token, choice) slot, then the affinity-weighted sum over k
-        y = y_sorted.index_select(0, inverse).view(T, k, H)
-        aff = self._chosen_affinities(expert_affinities, expert_index).to(y.dtype)
-        return torch.einsum("tkh,tk->th", y, aff)
+        # loop backend (default outside graph capture): one host read of the group sizes per layer,
+        # per-expert hipBLASLt GEMMs; grouped backend: the sync-free grouped kernel
+        bounds = ops.grouped_gemm.host_group_bounds(offs)
+        h = self.mlp_op._activation(ops.grouped_linear(x_sorted, w_gu, offs, bounds))
+        y_sorted = ops.grouped_linear(h, w_d, offs, bounds)    # [T*k, H] TP-partial
+        # un-permute each (token, choice) slot and take the affinity-weighted sum over k (one kernel)
+        aff = self._chosen_affinities(expert_affinities, expert_index)
+        return ops.moe_unpermute_combine(y_sorted, inverse, aff)
 
     def forward_all_experts(self, hidden_states, expert_affinities, expert_index):
         """Every token through every expert (reference semantics; used for tiny batches)."""

@@ -110,7 +110,10 @@ def _moe(E=8, k=2, H=512, I=768, dtype=torch.bfloat16):
     return MoE(r, mlps, return_router_logits=True)
 
 
-def test_dropless_moe_matches_fp32_and_has_no_host_sync():
+@pytest.mark.parametrize("backend", ["grouped", "loop"])
+def test_dropless_moe_matches_fp32_and_has_no_host_sync(backend, monkeypatch):
+    """Both expert-GEMM backends match fp32; the grouped one never reads a group size on the host."""
+    monkeypatch.setattr(ops.grouped_gemm, "MOE_GEMM", backend)
     _single()
     layer = _moe()
     ref_layer = _moe(dtype=torch.float32)               # same init, fp32, CPU reference path
@@ -122,7 +125,8 @@ def test_dropless_moe_matches_fp32_and_has_no_host_sync():
     xg = x.to(DEV).requires_grad_(True)
     xr = x.clone().requires_grad_(True)
     torch.cuda.synchronize()
-    torch.cuda.set_sync_debug_mode("error")               # any device->host sync raises
+    if backend == "grouped":
+        torch.cuda.set_sync_debug_mode("error")           # any device->host sync raises
     try:
         out, _ = layer(xg.to(torch.bfloat16))
         out.float().square().mean().backward()
@@ -138,3 +142,57 @@ def test_dropless_moe_matches_fp32_and_has_no_host_sync():
         g = dict(layer.named_parameters())[name].grad.float().cpu()
         g_ref = dict(ref_layer.named_parameters())[name].grad
         assert ((g - g_ref).abs().max() / g_ref.abs().max()).item() < 5e-2, name
+
+
+def test_grouped_linear_loop_backend_matches_grouped():
+    """NXD_MOE_GEMM=loop (per-expert hipBLASLt over host bounds) == the device-side grouped kernel:
+    forward, input gradient and fp32 weight gradient, ragged and empty groups included."""
+    import neuronx_distributed_llama3_2_amd.ops as ops
+
+    torch.manual_seed(0)
+    E, T, k, K, N = 6, 700, 2, 256, 384
+    idx = torch.randint(0, E - 1, (T, k), device="cuda")          # expert E-1 stays empty
+    order, inverse, offs = ops.moe_permutation(idx, E)
+    bounds = offs.tolist()
+    x = torch.randn(T * k, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(E, K, N, device="cuda") * 0.05).to(torch.bfloat16)
+    dy = torch.randn(T * k, N, device="cuda", dtype=torch.bfloat16)
+    outs = []
+    for b in (None, bounds):
+        xr = x.clone().requires_grad_(True)
+        wr = w.clone().requires_grad_(True)
+        y = ops.grouped_linear(xr, wr, offs, b)
+        y.backward(dy)
+        outs.append((y.float(), xr.grad.float(), wr.grad.float()))
+    for a, b in zip(*outs):
+        assert ((a - b).abs().max() / (b.abs().max() + 1e-6)).item() < 2e-2
+
+
+@pytest.mark.parametrize("T,k,H", [(513, 2, 4096), (64, 1, 1024), (300, 8, 2056)])
+def test_moe_unpermute_combine_and_dispatch_match_fp32(T, k, H):
+    """csrc/moe_combine.hip: un-permute + affinity-weighted combine (fwd: out, bwd: d ys and fp32
+    d aff) and the dispatch gather's backward (a gather-sum) against fp32 PyTorch."""
+    torch.manual_seed(3)
+    E = 8
+    idx = torch.stack([torch.randperm(E, device=DEV)[:k] for _ in range(T)])
+    order, inverse, offs = ops.moe_permutation(idx, E)
+    ys = torch.randn(T * k, H, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    aff = torch.rand(T, k, device=DEV).requires_grad_(True)
+    out = ops.moe_unpermute_combine(ys, inverse, aff)
+    dout = torch.randn(T, H, device=DEV).to(torch.bfloat16)
+    out.backward(dout)
+    ys_r = ys.detach().float().requires_grad_(True)
+    aff_r = aff.detach().clone().requires_grad_(True)
+    ref = torch.einsum("tkh,tk->th", ys_r.index_select(0, inverse).view(T, k, H), aff_r)
+    ref.backward(dout.float())
+    assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    assert (ys.grad.float() - ys_r.grad).abs().max().item() < 1e-2 * ys_r.grad.abs().max().item()
+    assert torch.allclose(aff.grad, aff_r.grad, rtol=1e-3, atol=1e-3 * aff_r.grad.abs().max().item())
+
+    x = torch.randn(T, H, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    xs = ops.moe_dispatch(x, order, inverse, k)
+    assert torch.equal(xs, x.detach().index_select(0, order // k))
+    dxs = torch.randn(T * k, H, device=DEV).to(torch.bfloat16)
+    xs.backward(dxs)
+    ref_dx = torch.zeros(T, H, device=DEV).index_add_(0, order // k, dxs.float())
+    assert (x.grad.float() - ref_dx).abs().max().item() < 1e-2 * ref_dx.abs().max().item()
