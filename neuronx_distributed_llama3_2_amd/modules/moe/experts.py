@@ -138,8 +138,8 @@ class ExpertMLPs(nn.Module):
         order, inverse, offs = ops.moe_permutation(expert_index, self.num_experts)
         x_sorted = ops.moe_dispatch(hidden_states, order, inverse, k)
         w_gu, w_d = self.mlp_op.gate_up_proj.weight, self.mlp_op.down_proj.weight
-        # loop backend (default outside graph capture): one host read of the group sizes per layer,
-        # per-expert hipBLASLt GEMMs; grouped backend: the sync-free grouped kernel
+        # grouped backend (default): the sync-free grouped kernel; NXD_MOE_GEMM=loop|auto: one host
+        # read of the group sizes per layer, per-expert hipBLASLt GEMMs (profiles/r2_moe_layer_v1.md)
         bounds = ops.grouped_gemm.host_group_bounds(offs)
         h = self.mlp_op._activation(ops.grouped_linear(x_sorted, w_gu, offs, bounds))
         y_sorted = ops.grouped_linear(h, w_d, offs, bounds)    # [T*k, H] TP-partial

@@ -19,15 +19,16 @@ import torch
 
 from ._ext import ext, use_native
 
-# "grouped": the device-side grouped kernel, no host sync (hipGraph-capturable).
+# "grouped" (default): the device-side grouped kernel, no host sync (hipGraph-capturable).
 # "loop": one hipBLASLt GEMM per expert (torch.matmul: its first heuristic -- the group sizes change
 # every step, so the in-process tuner of ops/gemm.py would re-time every call) over host-read group
 # sizes: one device->host sync per MoE layer, not capturable, but hipBLASLt's large-M tiles
 # (Mixtral shapes, TP=1: fwd 1.08 vs 0.55 PF/s, dgrad 0.85 vs 0.65 / 1.33 vs 0.58, wgrad 0.58 vs 0.40;
 # profiles/r2_moe_grouped_gemm_v1.jsonl; whole layer 37.0 vs 60.5 ms at 16k tokens,
 # profiles/r2_moe_layer_v1.md).
-# "auto" (default): the loop, except while a hipGraph is being captured (no host read possible).
-MOE_GEMM = os.environ.get("NXD_MOE_GEMM", "auto")
+# "auto": the loop, except while a hipGraph is being captured (no host read possible).
+# Default "grouped": the MoE forward stays free of device->host syncs unless the user opts in.
+MOE_GEMM = os.environ.get("NXD_MOE_GEMM", "grouped")
 
 
 def host_group_bounds(offs: torch.Tensor) -> Optional[List[int]]:
