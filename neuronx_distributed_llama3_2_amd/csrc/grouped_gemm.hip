@@ -13,9 +13,10 @@
 //   DGRAD dx[m, k]    = dy[m, :] . W[e][k, :]^T      A row-major [M][N],  B = W[e] stored [K][N] read as [n][k]
 //   WGRAD dW[e][k, n] (+)= sum_{m in e} x[m, k] dy[m, n]    A = x^T (stored [m][k]), B = dy stored [m][n]
 // Workgroup = 4 waves, 128 x 128 output tile (2 x 2 waves of 64 x 64 = 2 x 2 v_mfma_f32_32x32x16_bf16
-// tiles each), K-step 64, two LDS buffers (64 KiB) filled by register staging (loads for tile t+1
-// are in flight while tile t runs its 16 MFMAs per wave; zero-fill handles ragged rows and
-// k / n tails, which glds cannot).  Operands consumed along their contiguous axis are read with
+// tiles each), K-step 64, two LDS buffers (64 KiB): full reduction tiles go global -> LDS by
+// LDS-DMA (tile t+1 in flight while tile t runs its 16 MFMAs per wave), a ragged reduction tail
+// by zero-filling register staging; workgroups walk the tile grid in L2-sized bands
+// (band_raster).  Mixtral shapes: 0.55-0.74 -> 0.80-0.84 PF/s fwd / dgrad (profiles/r2_moe_layer_v1.md).  Operands consumed along their contiguous axis are read with
 // ds_read_b128 from a [row][64] image (16-B chunk XOR (row>>1)&7: conflict-free over 16 lanes);
 // operands stored reduction-major are read with the hardware transpose ds_read_b64_tr_b16 from a
 // [k][128] image (chunk XOR (k&3)<<2: the four rows of one transposed read and the two column
@@ -91,6 +92,41 @@ __device__ __forceinline__ void store_tr(char* img, const u32x4_t* v) {
   }
 }
 
+// LDS-DMA staging (global_load_lds_dwordx4: 1 KiB per wave-instruction, written lane-linearly at
+// M0): the XOR swizzle of the LDS images is applied to each lane's SOURCE address instead, so the
+// tile never passes through VGPRs or the ds_write path (whose VGPR->LDS transfer, ~79 B/clk/CU,
+// cost more LDS cycles per k-step than the MFMA fragment reads).  Issued from inline asm so the
+// compiler does not wait for it before every transposed LDS read; completion is a manual
+// vmcnt(0) before the k-step's barrier.  Rows / columns past the valid range re-read a valid
+// chunk (their outputs are never stored); reduction tails take the zero-filling VGPR path.
+typedef __attribute__((address_space(3))) char lds_char_t;
+__device__ __forceinline__ uint32_t lds_addr(const char* q) { return (uint32_t)(uintptr_t)(const lds_char_t*)q; }
+__device__ __forceinline__ void dma16(const void* src, uint32_t lds_dst) {
+  uint32_t sv;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(sv) : "v"(src), "s"(lds_dst) : "memory");
+}
+// [128 rows][64 k] row image: piece P (1 KiB) = rows 8P .. 8P + 7; lane l -> row 8P + l / 8, slot l % 8.
+__device__ __forceinline__ void dma_rows(uint32_t img, const uint16_t* base, int ld, int rows_valid, int k0) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = w * 4 + i, r = piece * 8 + (l >> 3), c = (l & 7) ^ ((r >> 1) & 7);
+    const int rr = min(r, rows_valid - 1);
+    dma16(base + (int64_t)rr * ld + k0 + 8 * c, __builtin_amdgcn_readfirstlane(img + piece * 1024));
+  }
+}
+// [64 k][128 cols] k-major image: piece P = k rows 4P .. 4P + 3; lane l -> k 4P + l / 16, slot l % 16.
+__device__ __forceinline__ void dma_tr(uint32_t img, const uint16_t* base, int ld, int c0, int C) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = w * 4 + i, k = piece * 4 + (l >> 4), c = (l & 15) ^ ((k & 3) << 2);
+    const int col = min(c0 + 8 * c, C - 8);
+    dma16(base + (int64_t)k * ld + col, __builtin_amdgcn_readfirstlane(img + piece * 1024));
+  }
+}
+
 // 32x32x16 operand fragment of rows [rbase, rbase + 32), k-step s: lane (r = l & 31, h = l >> 5)
 // needs element j = 0..7 at (row rbase + r, k 16 s + 8 h + j).
 __device__ __forceinline__ bf16x8_t frag_rows(const char* img, int rbase, int s) {
@@ -112,7 +148,19 @@ __device__ __forceinline__ bf16x8_t frag_tr(const char* img, int rbase, int s) {
   return __builtin_bit_cast(bf16x8_t, a8);
 }
 
-template <int MODE>
+// L2-aware raster: walk the (row tile, column tile) grid in bands of kBand row tiles, column-major
+// inside a band, so the workgroups resident on one XCD at a time (consecutive ids after
+// xcd_remap) share both A row tiles and B column tiles in that XCD's 4 MiB L2.  Row-major order
+// re-streamed the whole weight matrix W[e] from HBM once per row tile.
+constexpr int kBand = 8;
+__device__ __forceinline__ void band_raster(int id, int rows, int cols, int& r, int& c) {
+  const int band = id / (kBand * cols), within = id - band * kBand * cols;
+  const int h = min(kBand, rows - band * kBand);
+  r = band * kBand + within % h;
+  c = within / h;
+}
+
+template <int MODE, bool DMA>
 __global__ void __launch_bounds__(NT) grouped_gemm_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];   // [buf][A | B]
   const int nwg = gridDim.x;
@@ -125,15 +173,18 @@ __global__ void __launch_bounds__(NT) grouped_gemm_kernel(Params p) {
     const int per_e = p.r_tiles * p.n_tiles;
     e = id / per_e;
     const int rem = id - e * per_e;
-    row0 = (rem / p.n_tiles) * BM;            // rows of dW (= input features)
-    n0 = (rem % p.n_tiles) * BN;
+    int rt, ct;
+    band_raster(rem, p.r_tiles, p.n_tiles, rt, ct);
+    row0 = rt * BM;                           // rows of dW (= input features)
+    n0 = ct * BN;
     row_end = p.K;
     int lo = min(max(p.offs[e], 0), p.M), hi = min(max(p.offs[e + 1], 0), p.M);
     red0 = lo;
     red_end = max(hi, lo);
   } else {
-    const int slot = id / p.n_tiles;
-    n0 = (id % p.n_tiles) * BN;
+    int slot, ct;
+    band_raster(id, p.r_tiles, p.n_tiles, slot, ct);
+    n0 = ct * BN;
     // locate (expert, row tile) of this slot from the device offsets (E scalar iterations)
     int acc = 0, prev = 0;
     e = -1;
@@ -195,15 +246,39 @@ __global__ void __launch_bounds__(NT) grouped_gemm_kernel(Params p) {
     if (MODE == WGRAD) store_tr(ia, va); else store_rows(ia, va);
     if (MODE == DGRAD) store_rows(ib, vb); else store_tr(ib, vb);
   };
+  // full reduction tile t straight into LDS buffer `buf`
+  auto dma = [&](int t, int buf) {
+    const int k0 = red0 + t * BK;
+    const uint32_t ia = lds_addr(smem + buf * 2 * TILE_BYTES), ib = ia + TILE_BYTES;
+    if (MODE == WGRAD) {
+      dma_tr(ia, a_base + (int64_t)k0 * p.lda, p.lda, row0, p.K);
+      dma_tr(ib, b_base + (int64_t)k0 * p.ldb, p.ldb, n0, p.N);
+    } else if (MODE == FWD) {
+      dma_rows(ia, a_base, p.lda, rows_valid, k0);
+      dma_tr(ib, b_base + (int64_t)k0 * p.ldb, p.ldb, n0, p.N);
+    } else {
+      dma_rows(ia, a_base, p.lda, rows_valid, k0);
+      dma_rows(ib, b_base, p.ldb, p.N - n0, k0);
+    }
+  };
+  // tiles [0, n_full) cover BK full reduction steps; a ragged last tile is zero-filled through VGPRs
+  const int n_full = DMA ? (red_end - red0) / BK : 0;
 
   if (n_k > 0) {
-    load(0);
-    store(0);
+    if (n_full > 0) {
+      dma(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      load(0);
+      store(0);
+    }
     __syncthreads();
   }
   for (int t = 0; t < n_k; ++t) {
     const int buf = t & 1;
-    if (t + 1 < n_k) load(t + 1);
+    const bool next_dma = t + 1 < n_full, next_stage = t + 1 < n_k && !next_dma;
+    if (next_dma) dma(t + 1, buf ^ 1);
+    if (next_stage) load(t + 1);
     const char* ia = smem + buf * 2 * TILE_BYTES;
     const char* ib = ia + TILE_BYTES;
 #pragma unroll
@@ -219,7 +294,8 @@ __global__ void __launch_bounds__(NT) grouped_gemm_kernel(Params p) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < n_k) store(buf ^ 1);
+    if (next_stage) store(buf ^ 1);
+    if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
@@ -246,6 +322,15 @@ __global__ void __launch_bounds__(NT) grouped_gemm_kernel(Params p) {
     }
 }
 
+// NXD_GG_DMA=0 selects the VGPR-staged variant (A/B, tools/bench_grouped_gemm.py); read once.
+static bool use_dma() {
+  static const bool on = [] {
+    const char* e = getenv("NXD_GG_DMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 }  // namespace gg
 
 // mode 0 FWD:   a = x [M, K], b = W [E, K, N], c = y [M, N] bf16
@@ -270,7 +355,10 @@ int grouped_gemm_launch(int mode, const void* a, const void* b, void* c, const i
     if (M == 0) return 0;
     const int64_t nwg = (int64_t)p.n_tiles * p.r_tiles;
     if (nwg > INT32_MAX) return -2;
-    hipLaunchKernelGGL(gg::grouped_gemm_kernel<gg::FWD>, dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
+    if (gg::use_dma())
+      hipLaunchKernelGGL((gg::grouped_gemm_kernel<gg::FWD, true>), dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
+    else
+      hipLaunchKernelGGL((gg::grouped_gemm_kernel<gg::FWD, false>), dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
   } else if (mode == gg::DGRAD) {
     // dx [M, K] = dy [M, N] . W[e]^T : reduction over N, output columns K
     p.K = N; p.N = K; p.lda = N; p.ldb = N; p.ldc = K; p.b_estride = (int64_t)K * N;
@@ -279,14 +367,20 @@ int grouped_gemm_launch(int mode, const void* a, const void* b, void* c, const i
     if (M == 0) return 0;
     const int64_t nwg = (int64_t)p.n_tiles * p.r_tiles;
     if (nwg > INT32_MAX) return -2;
-    hipLaunchKernelGGL(gg::grouped_gemm_kernel<gg::DGRAD>, dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
+    if (gg::use_dma())
+      hipLaunchKernelGGL((gg::grouped_gemm_kernel<gg::DGRAD, true>), dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
+    else
+      hipLaunchKernelGGL((gg::grouped_gemm_kernel<gg::DGRAD, false>), dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
   } else if (mode == gg::WGRAD) {
     p.K = K; p.N = N; p.lda = K; p.ldb = N; p.ldc = N; p.c_estride = (int64_t)K * N;
     p.n_tiles = ceil_div(N, gg::BN);
     p.r_tiles = ceil_div(K, gg::BM);
     const int64_t nwg = (int64_t)p.n_tiles * p.r_tiles * E;
     if (nwg > INT32_MAX) return -2;
-    hipLaunchKernelGGL(gg::grouped_gemm_kernel<gg::WGRAD>, dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
+    if (gg::use_dma())
+      hipLaunchKernelGGL((gg::grouped_gemm_kernel<gg::WGRAD, true>), dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
+    else
+      hipLaunchKernelGGL((gg::grouped_gemm_kernel<gg::WGRAD, false>), dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
   } else {
     return -1;
   }
