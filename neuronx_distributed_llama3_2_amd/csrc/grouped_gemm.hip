@@ -301,6 +301,35 @@ __global__ void __launch_bounds__(NT) grouped_gemm_kernel(Params p) {
 
   // epilogue: acc element v of tile (i, j) is (row (v & 3) + 8 (v >> 2) + 4 (lane >> 5), col lane & 31)
   const int ccol = lane & 31, rsub = 4 * (lane >> 5);
+  if (MODE == WGRAD && p.accumulate) {
+    // dW += acc: batch the 32 fp32 reads of a tile row pair before any store (a load after a store
+    // to a possibly aliasing address is not hoisted, which serialised 64 HBM round trips per lane)
+    float* cbase = reinterpret_cast<float*>(p.c) + (int64_t)e * p.c_estride;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float old[2][16];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + 32 * j + ccol;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int r = wm * 64 + 32 * i + (v & 3) + 8 * (v >> 2) + rsub;
+          old[j][v] = (col < p.N && r < rows_valid) ? cbase[(int64_t)(row0 + r) * p.ldc + col] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + 32 * j + ccol;
+        if (col >= p.N) continue;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int r = wm * 64 + 32 * i + (v & 3) + 8 * (v >> 2) + rsub;
+          if (r < rows_valid) cbase[(int64_t)(row0 + r) * p.ldc + col] = old[j][v] + acc[i][j][v];
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
