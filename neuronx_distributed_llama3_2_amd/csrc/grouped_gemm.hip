@@ -45,6 +45,7 @@ struct Params {
   int64_t c_estride;    // elements between experts' dW (WGRAD)
   int n_tiles, r_tiles; // output tiles along N, and along rows (WGRAD: K / BM) or row-tile slots
   int accumulate;       // WGRAD: dW += (fp32 main_grad) instead of dW =
+  int band;             // row tiles per raster band (band_raster)
 };
 
 typedef __attribute__((address_space(3))) short4_t lds_short4_t;
@@ -152,8 +153,7 @@ __device__ __forceinline__ bf16x8_t frag_tr(const char* img, int rbase, int s) {
 // inside a band, so the workgroups resident on one XCD at a time (consecutive ids after
 // xcd_remap) share both A row tiles and B column tiles in that XCD's 4 MiB L2.  Row-major order
 // re-streamed the whole weight matrix W[e] from HBM once per row tile.
-constexpr int kBand = 8;
-__device__ __forceinline__ void band_raster(int id, int rows, int cols, int& r, int& c) {
+__device__ __forceinline__ void band_raster(int id, int rows, int cols, int kBand, int& r, int& c) {
   const int band = id / (kBand * cols), within = id - band * kBand * cols;
   const int h = min(kBand, rows - band * kBand);
   r = band * kBand + within % h;
@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(NT) grouped_gemm_kernel(Params p) {
     e = id / per_e;
     const int rem = id - e * per_e;
     int rt, ct;
-    band_raster(rem, p.r_tiles, p.n_tiles, rt, ct);
+    band_raster(rem, p.r_tiles, p.n_tiles, p.band, rt, ct);
     row0 = rt * BM;                           // rows of dW (= input features)
     n0 = ct * BN;
     row_end = p.K;
@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(NT) grouped_gemm_kernel(Params p) {
     red_end = max(hi, lo);
   } else {
     int slot, ct;
-    band_raster(id, p.r_tiles, p.n_tiles, slot, ct);
+    band_raster(id, p.r_tiles, p.n_tiles, p.band, slot, ct);
     n0 = ct * BN;
     // locate (expert, row tile) of this slot from the device offsets (E scalar iterations)
     int acc = 0, prev = 0;
@@ -352,6 +352,14 @@ __global__ void __launch_bounds__(NT) grouped_gemm_kernel(Params p) {
 }
 
 // NXD_GG_DMA=0 selects the VGPR-staged variant (A/B, tools/bench_grouped_gemm.py); read once.
+static int band_rows() {
+  static const int b = [] {
+    const char* e = getenv("NXD_GG_BAND");
+    const int v = e ? atoi(e) : 8;
+    return v > 0 ? v : 8;
+  }();
+  return b;
+}
 static bool use_dma() {
   static const bool on = [] {
     const char* e = getenv("NXD_GG_DMA");
@@ -377,6 +385,7 @@ int grouped_gemm_launch(int mode, const void* a, const void* b, void* c, const i
   p.E = E;
   p.M = M;
   p.accumulate = accumulate;
+  p.band = gg::band_rows();
   if (mode == gg::FWD) {
     p.K = K; p.N = N; p.lda = K; p.ldb = N; p.ldc = N; p.b_estride = (int64_t)K * N;
     p.n_tiles = ceil_div(N, gg::BN);
