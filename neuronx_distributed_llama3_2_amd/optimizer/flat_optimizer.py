@@ -186,13 +186,17 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
         for bi, b in enumerate(self.buffers):
             g = b.group
             beta1, beta2 = g["betas"]
+            fp32_params = b.buf.param_data.dtype == torch.float32   # e.g. MoE routers kept in fp32
             for (s, e, lo) in b.local:
                 n = e - s
                 ops.adamw_flat_(b.master[lo:lo + n], b.buf.grad_data[s:e], b.exp_avg[lo:lo + n], b.exp_avg_sq[lo:lo + n],
-                                b.buf.param_data[s:e], g["lr"], beta1, beta2, g["eps"], g["weight_decay"], self.step_count,
+                                None if fp32_params else b.buf.param_data[s:e], g["lr"], beta1, beta2, g["eps"],
+                                g["weight_decay"], self.step_count,
                                 grad_scale=coef, bias_correction=self.bias_correction,
                                 sr_seed=(((seed ^ (bi * 0x9E3779B1 + s)) & 0xFFFFFFFF) or 1) if seed else 0,
                                 hyper=hyper[b.group_index] if hyper is not None else None)
+                if fp32_params:
+                    b.buf.param_data[s:e].copy_(b.master[lo:lo + n])
         for b in self.buffers:
             b.buf.gather_params()
         return loss

@@ -196,3 +196,31 @@ def test_moe_unpermute_combine_and_dispatch_match_fp32(T, k, H):
     xs.backward(dxs)
     ref_dx = torch.zeros(T, H, device=DEV).index_add_(0, order // k, dxs.float())
     assert (x.grad.float() - ref_dx).abs().max().item() < 1e-2 * ref_dx.abs().max().item()
+
+
+def test_mixtral_trains_with_flat_adamw_fp32_router():
+    """Tiny Mixtral (fp32 router + bf16 experts) trains on the GPU under the flat fp32-master AdamW:
+    the fp32 parameter buffer takes the master copy (no bf16 write-back), loss goes down."""
+    from neuronx_distributed_llama3_2_amd.models.mixtral import MixtralForCausalLM, mixtral_config
+    from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW
+
+    _single()
+    torch.manual_seed(0)
+    cfg = mixtral_config("tiny", hidden_size=512, num_attention_heads=4, num_key_value_heads=2, intermediate_size=256)
+    model = MixtralForCausalLM(cfg, dtype=torch.bfloat16, device=torch.device(DEV))
+    model.train()
+    router = model.model.layers[0].block_sparse_moe.router.linear_router.weight
+    assert router.dtype == torch.float32
+    r0 = router.detach().clone()
+    opt = FlatMixedPrecisionAdamW(model.parameters(), lr=3e-3)
+    ids = torch.randint(0, cfg.vocab_size, (2, 256), device=DEV)
+    losses = []
+    for _ in range(6):
+        loss = model(ids, labels=ids).loss
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        losses.append(float(loss))
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert losses[-1] < losses[0]
+    assert router.dtype == torch.float32 and not torch.equal(router.detach(), r0)
