@@ -351,6 +351,195 @@ __global__ void __launch_bounds__(NT) grouped_gemm_kernel(Params p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Large-tile variant: 256 x 256 output tile per workgroup, 4 waves of 128 x 128 (4 x 4 MFMA tiles,
+// 256 fp32 accumulators per lane in AGPRs), BK 64, two 64 KiB LDS stages filled by LDS-DMA one
+// tile ahead, one workgroup per CU.  A k-step is 64 MFMAs per wave (~850 ns), long enough to
+// cover the LDS-DMA latency that bounds the 128 x 128 kernel (2 x its FLOP per byte staged).
+// Reduction tails read a zero chunk (g_zero16); rows / columns past the valid range re-read a
+// valid chunk (never stored).
+constexpr int BB = 256;                         // tile rows = tile cols
+constexpr int BIG_TILE = BB * BK * 2;           // 32 KiB per operand image
+__device__ __attribute__((aligned(16))) uint32_t g_zero16[4];   // zero-initialised device global
+
+// k-major [64 k][256 cols] image: 512-B rows, chunk XOR (k & 3) << 2 (as tr_img)
+__device__ __forceinline__ int trb_img(int k, int c) { return k * 512 + 16 * (c ^ ((k & 3) << 2)); }
+__device__ __forceinline__ bf16x8_t frag_trb(const char* img, int rbase, int s) {
+  const int l = threadIdx.x & 63, g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const int h = g >> 1;
+  const int col = rbase + 16 * (g & 1) + 4 * p;
+  const int k = 16 * s + 8 * h + q;
+  const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_short4_t*)(img + trb_img(k, col >> 3) + 8 * (p & 1)));
+  const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_short4_t*)(img + trb_img(k + 4, col >> 3) + 8 * (p & 1)));
+  const short __attribute__((ext_vector_type(8))) a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, a8);
+}
+// [256 rows][64 k] row image (row_img): piece P = rows 8P .. 8P + 7, 8 pieces per wave
+__device__ __forceinline__ void dma_rows_big(uint32_t img, const uint16_t* base, int ld, int rows_valid, int k0, int k_end) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int piece = w * 8 + i, r = piece * 8 + (l >> 3), c = (l & 7) ^ ((r >> 1) & 7);
+    const int rr = min(r, rows_valid - 1), k = k0 + 8 * c;
+    const void* src = k < k_end ? (const void*)(base + (int64_t)rr * ld + k) : (const void*)g_zero16;
+    dma16(src, __builtin_amdgcn_readfirstlane(img + piece * 1024));
+  }
+}
+// trb image: piece P = k rows 2P, 2P + 1; lane l -> k 2P + l / 32, slot l % 32
+__device__ __forceinline__ void dma_tr_big(uint32_t img, const uint16_t* base, int ld, int c0, int C, int k_valid) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int piece = w * 8 + i, k = piece * 2 + (l >> 5), c = (l & 31) ^ ((k & 3) << 2);
+    const int col = min(c0 + 8 * c, C - 8);
+    const void* src = k < k_valid ? (const void*)(base + (int64_t)k * ld + col) : (const void*)g_zero16;
+    dma16(src, __builtin_amdgcn_readfirstlane(img + piece * 1024));
+  }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(NT, 1) grouped_gemm_big_kernel(Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * BIG_TILE];   // [stage][A | B], 128 KiB
+  const int nwg = gridDim.x;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  int e = 0, row0 = 0, row_end = 0, n0 = 0, red0 = 0, red_end = 0;
+  if (MODE == WGRAD) {
+    const int per_e = p.r_tiles * p.n_tiles;
+    e = id / per_e;
+    int rt, ct;
+    band_raster(id - e * per_e, p.r_tiles, p.n_tiles, p.band, rt, ct);
+    row0 = rt * BB;
+    n0 = ct * BB;
+    row_end = p.K;
+    const int lo = min(max(p.offs[e], 0), p.M), hi = min(max(p.offs[e + 1], 0), p.M);
+    red0 = lo;
+    red_end = max(hi, lo);
+  } else {
+    int slot, ct;
+    band_raster(id, p.r_tiles, p.n_tiles, p.band, slot, ct);
+    n0 = ct * BB;
+    int acc_t = 0, prev = 0;
+    e = -1;
+    for (int x = 0; x < p.E; ++x) {
+      const int lo = min(max(p.offs[x], prev), p.M), hi = min(max(p.offs[x + 1], lo), p.M);
+      prev = hi;
+      const int tiles = (hi - lo + BB - 1) / BB;
+      if (slot < acc_t + tiles) {
+        e = x;
+        row0 = lo + (slot - acc_t) * BB;
+        row_end = hi;
+        break;
+      }
+      acc_t += tiles;
+    }
+    if (e < 0) return;
+    red0 = 0;
+    red_end = p.K;
+  }
+  const uint16_t* a_base;
+  const uint16_t* b_base;
+  if (MODE == FWD) {
+    a_base = p.a + (int64_t)row0 * p.lda;
+    b_base = p.b + (int64_t)e * p.b_estride;
+  } else if (MODE == DGRAD) {
+    a_base = p.a + (int64_t)row0 * p.lda;
+    b_base = p.b + (int64_t)e * p.b_estride + (int64_t)n0 * p.ldb;
+  } else {
+    a_base = p.a;
+    b_base = p.b;
+  }
+  const int rows_valid = row_end - row0;
+
+  f32x16_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x16_t{0};
+
+  const int n_k = (red_end - red0 + BK - 1) / BK;
+  auto issue = [&](int t, int buf) {
+    const int k0 = red0 + t * BK;
+    const uint32_t ia = lds_addr(smem + buf * 2 * BIG_TILE), ib = ia + BIG_TILE;
+    if (MODE == WGRAD) {
+      dma_tr_big(ia, a_base + (int64_t)k0 * p.lda, p.lda, row0, p.K, red_end - k0);
+      dma_tr_big(ib, b_base + (int64_t)k0 * p.ldb, p.ldb, n0, p.N, red_end - k0);
+    } else if (MODE == FWD) {
+      dma_rows_big(ia, a_base, p.lda, rows_valid, k0, p.K);
+      dma_tr_big(ib, b_base + (int64_t)k0 * p.ldb, p.ldb, n0, p.N, p.K - k0);
+    } else {
+      dma_rows_big(ia, a_base, p.lda, rows_valid, k0, p.K);
+      dma_rows_big(ib, b_base, p.ldb, p.N - n0, k0, p.K);
+    }
+  };
+  if (n_k > 0) {
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int t = 0; t < n_k; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < n_k) issue(t + 1, buf ^ 1);
+    const char* ia = smem + buf * 2 * BIG_TILE;
+    const char* ib = ia + BIG_TILE;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8_t af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i] = (MODE == WGRAD) ? frag_trb(ia, wm * 128 + 32 * i, s) : frag_rows(ia, wm * 128 + 32 * i, s);
+        bfr[i] = (MODE == DGRAD) ? frag_rows(ib, wn * 128 + 32 * i, s) : frag_trb(ib, wn * 128 + 32 * i, s);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  const int ccol = lane & 31, rsub = 4 * (lane >> 5);
+  if (MODE == WGRAD) {
+    float* cbase = reinterpret_cast<float*>(p.c) + (int64_t)e * p.c_estride;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {   // 16 reads in flight before the tile's 16 stores
+        const int col = n0 + wn * 128 + 32 * j + ccol;
+        float old[16];
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int r = wm * 128 + 32 * i + (v & 3) + 8 * (v >> 2) + rsub;
+          old[v] = (p.accumulate && col < p.N && r < rows_valid) ? cbase[(int64_t)(row0 + r) * p.ldc + col] : 0.f;
+        }
+        if (col >= p.N) continue;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int r = wm * 128 + 32 * i + (v & 3) + 8 * (v >> 2) + rsub;
+          if (r < rows_valid) cbase[(int64_t)(row0 + r) * p.ldc + col] = old[v] + acc[i][j][v];
+        }
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn * 128 + 32 * j + ccol;
+        if (col >= p.N) continue;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int r = wm * 128 + 32 * i + (v & 3) + 8 * (v >> 2) + rsub;
+          if (r < rows_valid) reinterpret_cast<uint16_t*>(p.c)[(int64_t)(row0 + r) * p.ldc + col] = f2bf(acc[i][j][v]);
+        }
+      }
+  }
+}
+
 // NXD_GG_DMA=0 selects the VGPR-staged variant (A/B, tools/bench_grouped_gemm.py); read once.
 static int band_rows() {
   static const int b = [] {
@@ -359,6 +548,14 @@ static int band_rows() {
     return v > 0 ? v : 8;
   }();
   return b;
+}
+// NXD_GG_BIG=1: 256 x 256 tiles (grouped_gemm_big_kernel); read once.
+static bool use_big() {
+  static const bool on = [] {
+    const char* e = getenv("NXD_GG_BIG");
+    return e && e[0] == '1';
+  }();
+  return on;
 }
 static bool use_dma() {
   static const bool on = [] {
@@ -386,6 +583,36 @@ int grouped_gemm_launch(int mode, const void* a, const void* b, void* c, const i
   p.M = M;
   p.accumulate = accumulate;
   p.band = gg::band_rows();
+  if (gg::use_big()) {
+    constexpr int T = gg::BB;
+    if (mode == gg::FWD || mode == gg::DGRAD) {
+      if (mode == gg::FWD) {
+        p.K = K; p.N = N; p.lda = K; p.ldb = N; p.ldc = N;
+      } else {
+        p.K = N; p.N = K; p.lda = N; p.ldb = N; p.ldc = K;
+      }
+      p.b_estride = (int64_t)K * N;
+      p.n_tiles = ceil_div(p.N, T);
+      p.r_tiles = ceil_div(M, T) + E;
+      if (M == 0) return 0;
+      const int64_t nwg = (int64_t)p.n_tiles * p.r_tiles;
+      if (nwg > INT32_MAX) return -2;
+      if (mode == gg::FWD)
+        hipLaunchKernelGGL(gg::grouped_gemm_big_kernel<gg::FWD>, dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
+      else
+        hipLaunchKernelGGL(gg::grouped_gemm_big_kernel<gg::DGRAD>, dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
+    } else if (mode == gg::WGRAD) {
+      p.K = K; p.N = N; p.lda = K; p.ldb = N; p.ldc = N; p.c_estride = (int64_t)K * N;
+      p.n_tiles = ceil_div(N, T);
+      p.r_tiles = ceil_div(K, T);
+      const int64_t nwg = (int64_t)p.n_tiles * p.r_tiles * E;
+      if (nwg > INT32_MAX) return -2;
+      hipLaunchKernelGGL(gg::grouped_gemm_big_kernel<gg::WGRAD>, dim3((unsigned)nwg), dim3(gg::NT), 0, stream, p);
+    } else {
+      return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+  }
   if (mode == gg::FWD) {
     p.K = K; p.N = N; p.lda = K; p.ldb = N; p.ldc = N; p.b_estride = (int64_t)K * N;
     p.n_tiles = ceil_div(N, gg::BN);
