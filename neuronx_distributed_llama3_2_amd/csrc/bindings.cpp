@@ -51,6 +51,7 @@ int expert_gemv_launch(const void*, int64_t, const void*, int64_t, int64_t, cons
                        int, int, hipStream_t);
 void dgemv_set_knob(int, int);
 void decode_attn_set_v2(int);
+void decode_attn_set_prefetch(const void*, int64_t, const void*, int64_t, int);
 int dgemv_launch(int, const void*, int64_t, const void*, float, const void*, int64_t, void*, int64_t, int, int, int, int,
                  int, int, const float*, const float*, const int64_t*, int, void*, void*, int64_t, int64_t, int64_t,
                  const int*, int, int, hipStream_t);
@@ -394,6 +395,21 @@ int* decode_counters(int dev, int64_t n) {
   return bufs[dev].data_ptr<int>();
 }
 
+// Arm the NEXT decode_attn launch with up to two weight ranges to stream into the Infinity Cache
+// from spare workgroups of its grid (o_proj and the head of gate_up in the fused decode layer).
+void decode_attn_prefetch(c10::optional<at::Tensor> a, int64_t a_bytes, c10::optional<at::Tensor> b, int64_t b_bytes,
+                          int64_t wgs) {
+  auto rng = [](const c10::optional<at::Tensor>& t, int64_t n) -> std::pair<const void*, int64_t> {
+    if (!t.has_value() || !t->defined()) return {nullptr, 0};
+    check_cuda(*t, "prefetch range");
+    TORCH_CHECK(t->is_contiguous(), "prefetch range must be contiguous");
+    const int64_t total = t->numel() * t->element_size();
+    return {t->data_ptr(), std::max<int64_t>(0, std::min(n < 0 ? total : n, total))};
+  };
+  const auto ra = rng(a, a_bytes), rb = rng(b, b_bytes);
+  nxd::decode_attn_set_prefetch(ra.first, ra.second, rb.first, rb.second, (int)wgs);
+}
+
 void decode_attn(at::Tensor q, at::Tensor kc, at::Tensor vc, c10::optional<at::Tensor> cache_idx, at::Tensor seq_len,
                  at::Tensor out, double scale, int64_t nsplit) {
   int64_t qs[3], os[3];
@@ -431,6 +447,7 @@ void decode_attn(at::Tensor q, at::Tensor kc, at::Tensor vc, c10::optional<at::T
                                    po.data_ptr<float>(), pm.data_ptr<float>(), pl.data_ptr<float>(), counters, out.data_ptr(),
                                    os, B, T, Hq, Hkv, D, (int)nsplit, (float)scale, cur_stream()),
            "decode_attn");
+  nxd::decode_attn_set_prefetch(nullptr, 0, nullptr, 0, 0);   // armed ranges never outlive one call
 }
 
 // k, v: [B, T, Hkv, D] strided; caches [Bc, Hkv, Lmax, D]; pos: int32 [B] position of token 0
@@ -801,6 +818,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("decode_attn", &decode_attn);
+  m.def("decode_attn_prefetch", &decode_attn_prefetch);
   m.def("kv_cache_write", &kv_cache_write);
   m.def("argmax_rows", &argmax_rows);
   m.def("greedy_advance", &greedy_advance);

@@ -36,7 +36,32 @@ struct Params {
   float* pl;
   int B, T, Hq, Hkv, nsplit;
   float scale_log2;   // softmax scale * log2(e)
+  // weight prefetch riding on the (tiny) attention grid: workgroups >= attn_wgs stream the two
+  // byte ranges through the memory hierarchy so the next projections (o_proj, gate_up) find them
+  // in the Infinity Cache instead of cold HBM; the attention itself leaves HBM idle
+  const u32x4_t* pf[2];
+  int64_t pf_n16[2];   // 16-byte chunks per range
+  int attn_wgs;
 };
+
+// Prefetch workgroup body: 4 independent 16-B loads in flight per lane, folded into one value that
+// is stored only under a condition the host never creates (pf_n16[0] < 0), so the loads stay live.
+__device__ __forceinline__ void prefetch_body(const Params& p, int wg, int nwg) {
+  uint32_t acc = 0;
+  const int64_t stride = (int64_t)nwg * blockDim.x;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const u32x4_t* base = p.pf[r];
+    const int64_t n = p.pf_n16[r];
+    int64_t i = (int64_t)wg * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+      const u32x4_t a = base[i], b = base[i + stride], c = base[i + 2 * stride], d = base[i + 3 * stride];
+      acc ^= a[0] ^ b[1] ^ c[2] ^ d[3];
+    }
+    for (; i < n; i += stride) acc ^= base[i][0];
+  }
+  if (p.pf_n16[0] < 0) p.pm[threadIdx.x] = __uint_as_float(acc);
+}
 
 typedef __attribute__((address_space(3))) short4_t lds_s4_t;
 typedef short short8_t __attribute__((ext_vector_type(8)));
@@ -54,6 +79,10 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
   float* red_m = red_o + NWV * 16 * D;                                          // [NWV][16]
   float* red_l = red_m + NWV * 16;
 
+  if ((int)blockIdx.x >= p.attn_wgs) {
+    prefetch_body(p, blockIdx.x - p.attn_wgs, gridDim.x - p.attn_wgs);
+    return;
+  }
   const int split = blockIdx.x % p.nsplit;
   const int bh = blockIdx.x / p.nsplit;
   const int b = bh / p.Hkv, hkv = bh % p.Hkv;
@@ -225,7 +254,20 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
   }
 }
 
+// Pending prefetch of the next decode_attn2 launch (set by decode_attn_set_prefetch, consumed by
+// one launch: graph capture records the kernel arguments by value, so every captured layer keeps
+// its own ranges).
+static const void* g_pf[2] = {nullptr, nullptr};
+static int64_t g_pf_bytes[2] = {0, 0};
+static int g_pf_wgs = 0;
+
 }  // namespace dattn
+
+void decode_attn_set_prefetch(const void* a, int64_t a_bytes, const void* b, int64_t b_bytes, int wgs) {
+  dattn::g_pf[0] = a; dattn::g_pf_bytes[0] = a ? a_bytes : 0;
+  dattn::g_pf[1] = b; dattn::g_pf_bytes[1] = b ? b_bytes : 0;
+  dattn::g_pf_wgs = wgs;
+}
 
 // Returns -1 when the shape is not covered (caller falls back to the 128-key-chunk kernel).
 int decode_attn2_launch(const void* q, const int64_t* qs, const void* kc, const void* vc, const int64_t* cs,
@@ -249,7 +291,18 @@ int decode_attn2_launch(const void* q, const int64_t* qs, const void* kc, const 
   // D = 64: 8 waves (<= 2 chunks each per 1024-key split); D = 128: 4 waves (LDS: V tiles + merge)
   const int nwv = D == 64 ? 8 : 4;
   const size_t lds = (size_t)nwv * dattn::KB * D * 2 + (size_t)nwv * 16 * D * 4 + (size_t)2 * nwv * 16 * 4;
-  const dim3 grid(B * Hkv * p.nsplit), block(64 * nwv);
+  p.attn_wgs = B * Hkv * p.nsplit;
+  int pf_wgs = 0;
+  for (int r = 0; r < 2; ++r) {
+    // 16-B aligned start, whole chunks only (a prefetch never needs the ragged tail)
+    const bool ok = dattn::g_pf[r] && (reinterpret_cast<uintptr_t>(dattn::g_pf[r]) & 15) == 0 && dattn::g_pf_bytes[r] >= 16;
+    p.pf[r] = ok ? static_cast<const u32x4_t*>(dattn::g_pf[r]) : nullptr;
+    p.pf_n16[r] = ok ? dattn::g_pf_bytes[r] / 16 : 0;
+    if (ok) pf_wgs = dattn::g_pf_wgs > 0 ? dattn::g_pf_wgs : 256;
+  }
+  dattn::g_pf[0] = dattn::g_pf[1] = nullptr;
+  dattn::g_pf_bytes[0] = dattn::g_pf_bytes[1] = 0;
+  const dim3 grid(p.attn_wgs + pf_wgs), block(64 * nwv);
   if (D == 64) {
     (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<64, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((dattn::attn_kernel<64, 8>), grid, block, lds, stream, p);

@@ -34,6 +34,11 @@ from ..ops.gemv import skinny_linear
 from ..parallel_layers import parallel_state as ps
 from ..parallel_layers.parallel_state import get_tensor_model_parallel_size
 
+# Fused decode: MiB of the gate_up weight (after all of o_proj) that the attention launch streams
+# into the Infinity Cache from spare workgroups (0 disables), and how many workgroups do it.
+_PREFETCH_MB = float(os.environ.get("NXD_DECODE_PREFETCH_MB", "0"))
+_PREFETCH_WGS = int(os.environ.get("NXD_DECODE_PREFETCH_WGS", "256"))
+
 
 class DecoderInferenceMixin:
     """Inference forward of a decoder-only causal LM whose modules follow the framework's training
@@ -181,10 +186,14 @@ class DecoderInferenceMixin:
             C.dgemv(3, res, layer.input_layernorm.weight, self.eps, w_qkv, qkv, nq, nkv, D, cos_t, sin_t, pos, T,
                     kc, vc, sid32)
             q = qkv.view(B, T, nq + 2 * nkv, D)[:, :, :nq]
+            ln2, w_gu, w_d = self._fused_ffn_weights(layer)
+            if _PREFETCH_MB > 0:
+                # spare workgroups of the attention launch pull o_proj and the head of gate_up into
+                # the Infinity Cache while the (latency-bound) attention leaves HBM idle
+                C.decode_attn_prefetch(attn.o_proj.weight, -1, w_gu, int(_PREFETCH_MB * 2**20), _PREFETCH_WGS)
             o = ops.decode_attention(q, kc, vc, cache_len, sid32)
             C.dgemv(1, o.reshape(M, nq * D), None, 0.0, attn.o_proj.weight, res, 0, 0, 0, None, None, None, 1,
                     None, None, None)                                   # res += o_proj(o)
-            ln2, w_gu, w_d = self._fused_ffn_weights(layer)
             a = torch.empty((M, w_d.shape[1]), dtype=res.dtype, device=res.device)
             C.dgemv(2, res, ln2, self.eps, w_gu, a, 0, 0, 0, None, None, None, 1, None, None, None)  # norm+SwiGLU
             C.dgemv(1, a, None, 0.0, w_d, res, 0, 0, 0, None, None, None, 1, None, None, None)   # res += down(a)

@@ -220,6 +220,28 @@ def test_fused_decode_matches_unfused(hidden, heads):
     assert ((lf - lu).abs().max() / lu.abs().max()).item() < 3e-2
 
 
+def test_fused_decode_weight_prefetch_is_exact(monkeypatch):
+    """Spare attention workgroups streaming o_proj / gate_up into the Infinity Cache only read:
+    decode tokens and logits are bit-identical with and without the prefetch."""
+    from transformers import LlamaConfig, LlamaForCausalLM as HF
+    from neuronx_distributed_llama3_2_amd.inference import model_base
+
+    cfg = LlamaConfig(hidden_size=512, intermediate_size=1024, num_hidden_layers=2, num_attention_heads=8,
+                      num_key_value_heads=2, vocab_size=1000, max_position_embeddings=1024, rms_norm_eps=1e-5,
+                      rope_theta=500000.0, tie_word_embeddings=True, eos_token_id=2)
+    torch.manual_seed(0)
+    sd = {k: v.detach().clone() for k, v in HF(cfg).state_dict().items()}
+    torch.manual_seed(5)
+    ids = torch.randint(3, cfg.vocab_size, (2, 33))
+    outs = []
+    for mb in (0.0, 64.0):   # 64 MiB clamps to the whole gate_up weight
+        monkeypatch.setattr(model_base, "_PREFETCH_MB", mb)
+        m = _model(cfg, sd, torch.bfloat16, graphs=True, steps=4, device=torch.device("cuda"))
+        outs.append(m.generate(ids, max_new_tokens=16, eos_token_id=-1).cpu())
+        assert m.model._decode_fused_ok is True
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_weight_layout_pass_on_gpu(hf_sd):
     """Measured layout pass at the prefill size: every weight gets a layout, packed copies are
     K-major, and prefill logits match the stored-layout model (forced-packed too)."""
