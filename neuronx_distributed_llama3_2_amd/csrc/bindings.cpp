@@ -25,6 +25,7 @@ int rope_inplace_launch(void*, int64_t, int64_t, int, int, int, const float*, co
                         int64_t, float, hipStream_t);
 int swiglu_fwd_launch(const void*, void*, int64_t, int, hipStream_t);
 int swiglu_bwd_launch(const void*, const void*, void*, int64_t, int, hipStream_t);
+int swiglu_bwd_dual_launch(const void*, const void*, void*, void*, int64_t, int, hipStream_t);
 int xent_stats_launch(const void*, int, const int64_t*, float*, int64_t, int, int64_t, int64_t, hipStream_t);
 int xent_bwd_launch(const void*, int, const int64_t*, const float*, void*, int64_t, int, int64_t, int64_t, int64_t, float,
                     int64_t, hipStream_t);
@@ -253,6 +254,24 @@ void swiglu_bwd(at::Tensor gu, at::Tensor dh, at::Tensor dgu) {
   TORCH_CHECK(dh.numel() * 2 == gu.numel() && dgu.numel() == gu.numel(), "shape mismatch");
   check_rc(nxd::swiglu_bwd_launch(gu.data_ptr(), dh.data_ptr(), dgu.data_ptr(), gu.numel() / I2, (int)(I2 / 2), cur_stream()),
            "swiglu_bwd");
+}
+
+// dgu and its transpose dgu_t [2I, rows] (contiguous) in one kernel; rows and I multiples of 64.
+void swiglu_bwd_dual(at::Tensor gu, at::Tensor dh, at::Tensor dgu, at::Tensor dgu_t) {
+  const int64_t I2 = gu.size(-1);
+  rows_check(gu, "gate_up", I2);
+  rows_check(dh, "dh", I2 / 2);
+  rows_check(dgu, "dgu", I2);
+  TORCH_CHECK(dh.numel() * 2 == gu.numel() && dgu.numel() == gu.numel(), "shape mismatch");
+  const int64_t N = gu.numel() / I2;
+  check_bf16(dgu_t, "dgu_t");
+  TORCH_CHECK(dgu_t.dim() == 2 && dgu_t.size(0) == I2 && dgu_t.size(1) == N && dgu_t.is_contiguous(),
+              "dgu_t must be contiguous [2I, rows]");
+  TORCH_CHECK(N % 64 == 0 && (I2 / 2) % 64 == 0, "swiglu_bwd_dual: rows and I must be multiples of 64");
+  check_aligned16(dgu_t, "dgu_t");
+  check_rc(nxd::swiglu_bwd_dual_launch(gu.data_ptr(), dh.data_ptr(), dgu.data_ptr(), dgu_t.data_ptr(), N, (int)(I2 / 2),
+                                       cur_stream()),
+           "swiglu_bwd_dual");
 }
 
 void logits_check(const at::Tensor& x) {
@@ -809,6 +828,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("transpose_bf16", &transpose_bf16);
   m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("swiglu_bwd_dual", &swiglu_bwd_dual);
   m.def("xent_stats", &xent_stats);
   m.def("xent_bwd", &xent_bwd);
   m.def("flat_reduce", &flat_reduce);

@@ -51,6 +51,60 @@ __global__ void __launch_bounds__(256) bwd_kernel(const uint16_t* __restrict__ g
   }
 }
 
+// Backward with a second, transposed copy of d(gate_up) for the weight gradient: the gate_up
+// wgrad runs as a TN GEMM on T-contiguous operands, which otherwise costs a separate transpose of
+// the [T, 2I] gradient (read + write of the largest activation gradient of the layer).  Each
+// workgroup owns a 64-row x 64-column tile of the gate and up halves: the row-major result is
+// written straight from registers, the transposed one goes through LDS and leaves as 16-byte
+// vectors of 8 consecutive rows (tokens).  N % 64 == 0 and I % 64 == 0 (checked by the launcher).
+constexpr int TT = 64;
+constexpr int LDT = TT + 8;   // LDS row stride (elements): 16-B aligned rows, offset banks
+
+__global__ void __launch_bounds__(256) bwd_dual_kernel(const uint16_t* __restrict__ gu, const uint16_t* __restrict__ dh,
+                                                       uint16_t* __restrict__ dgu, uint16_t* __restrict__ dgu_t, int64_t N,
+                                                       int I) {
+  __shared__ __attribute__((aligned(16))) uint16_t sdg[TT * LDT];
+  __shared__ __attribute__((aligned(16))) uint16_t sdu[TT * LDT];
+  const int tid = threadIdx.x;
+  const int col0 = blockIdx.x * TT;
+  const int64_t row0 = (int64_t)blockIdx.y * TT;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int v = tid + 256 * it, r = v >> 3, c = (v & 7) * 8;
+    const int64_t row = row0 + r;
+    const uint16_t* src = gu + row * 2 * I + col0 + c;
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(*reinterpret_cast<const u32x4_t*>(src), g);
+    unpack8(*reinterpret_cast<const u32x4_t*>(src + I), u);
+    unpack8(*reinterpret_cast<const u32x4_t*>(dh + row * I + col0 + c), d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s = sigm(g[j]);
+      du[j] = d[j] * g[j] * s;
+      dg[j] = d[j] * u[j] * s * (1.f + g[j] * (1.f - s));
+    }
+    const u32x4_t pg = pack8(dg), pu = pack8(du);
+    uint16_t* dst = dgu + row * 2 * I + col0 + c;
+    *reinterpret_cast<u32x4_t*>(dst) = pg;
+    *reinterpret_cast<u32x4_t*>(dst + I) = pu;
+    *reinterpret_cast<u32x4_t*>(sdg + r * LDT + c) = pg;
+    *reinterpret_cast<u32x4_t*>(sdu + r * LDT + c) = pu;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int v = tid + 256 * it, c = v >> 3, r = (v & 7) * 8;   // column c, tokens r .. r + 7
+    uint32_t wg[4], wu[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      wg[j] = (uint32_t)sdg[(r + 2 * j) * LDT + c] | ((uint32_t)sdg[(r + 2 * j + 1) * LDT + c] << 16);
+      wu[j] = (uint32_t)sdu[(r + 2 * j) * LDT + c] | ((uint32_t)sdu[(r + 2 * j + 1) * LDT + c] << 16);
+    }
+    *reinterpret_cast<u32x4_t*>(dgu_t + (int64_t)(col0 + c) * N + row0 + r) = u32x4_t{wg[0], wg[1], wg[2], wg[3]};
+    *reinterpret_cast<u32x4_t*>(dgu_t + (int64_t)(I + col0 + c) * N + row0 + r) = u32x4_t{wu[0], wu[1], wu[2], wu[3]};
+  }
+}
+
 }  // namespace swiglu
 
 static inline dim3 row_grid(int64_t N, int I) {
@@ -73,6 +127,16 @@ int swiglu_bwd_launch(const void* gu, const void* dh, void* dgu, int64_t N, int 
   if (nv == 0) return 0;
   hipLaunchKernelGGL(swiglu::bwd_kernel, row_grid(N, I), dim3(256), 0, stream, (const uint16_t*)gu, (const uint16_t*)dh,
                      (uint16_t*)dgu, N, I);
+  return (int)hipGetLastError();
+}
+
+// dgu [N, 2I] row-major and dgu_t [2I, N] (its transpose) in one pass; -1 if the shape is not tiled.
+int swiglu_bwd_dual_launch(const void* gu, const void* dh, void* dgu, void* dgu_t, int64_t N, int I, hipStream_t stream) {
+  if (I % swiglu::TT || N % swiglu::TT || N / swiglu::TT > 65535) return -1;
+  if (N == 0) return 0;
+  const dim3 grid((unsigned)(I / swiglu::TT), (unsigned)(N / swiglu::TT));
+  hipLaunchKernelGGL(swiglu::bwd_dual_kernel, grid, dim3(256), 0, stream, (const uint16_t*)gu, (const uint16_t*)dh,
+                     (uint16_t*)dgu, (uint16_t*)dgu_t, N, I);
   return (int)hipGetLastError();
 }
 

@@ -1,6 +1,14 @@
-"""SwiGLU on a fused gate_up projection (csrc/swiglu.hip)."""
+"""SwiGLU on a fused gate_up projection (csrc/swiglu.hip).
+
+The backward also writes d(gate_up) transposed ([2I, T], token-contiguous) when the shape tiles by
+64: the gate_up weight gradient runs as a TN GEMM on T-contiguous operands (ops/gemm.py), and the
+transposed copy — attached to the returned gradient as `_nxd_t` — replaces the separate transpose
+of the layer's largest activation gradient.  NXD_SWIGLU_DUAL=0 disables it.
+"""
 
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn.functional as F
@@ -11,6 +19,9 @@ from ._ext import ext, use_native
 def swiglu_reference(gu: torch.Tensor) -> torch.Tensor:
     g, u = gu.float().chunk(2, dim=-1)
     return (F.silu(g) * u).to(gu.dtype)
+
+
+_DUAL = os.environ.get("NXD_SWIGLU_DUAL", "1") == "1"
 
 
 class SwiGLUFunc(torch.autograd.Function):
@@ -26,6 +37,13 @@ class SwiGLUFunc(torch.autograd.Function):
     def backward(ctx, dh):
         (gu,) = ctx.saved_tensors
         dgu = torch.empty_like(gu)
+        I2 = gu.shape[-1]
+        rows = gu.numel() // I2 if I2 else 0
+        if _DUAL and rows and rows % 64 == 0 and (I2 // 2) % 64 == 0:
+            dgu_t = torch.empty((I2, rows), dtype=gu.dtype, device=gu.device)
+            ext().swiglu_bwd_dual(gu, dh.contiguous(), dgu, dgu_t)
+            dgu._nxd_t = dgu_t
+            return dgu
         ext().swiglu_bwd(gu, dh.contiguous(), dgu)
         return dgu
 

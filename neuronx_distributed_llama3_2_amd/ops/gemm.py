@@ -79,8 +79,11 @@ def _wgrad_scratch(n: int, dtype, device, tag: str = "") -> torch.Tensor:
     return t[:n]
 
 
-def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor) -> None:
+def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor, go_t: torch.Tensor = None) -> None:
     """mg [N, K] (fp32) += go2[T, N]^T @ x2[T, K].
+
+    `go_t`: optional contiguous [N, T] copy of go2 already written by its producer (the SwiGLU
+    backward), used instead of transposing go2 when the TN layout is taken.
 
     Default: one hipBLASLt GEMM with fp32 C/D and beta = 1.  NXD_WGRAD_BF16=1: bf16-output GEMM
     into a reused scratch, then an fp32 add (the per-micro-batch weight gradient is rounded to
@@ -91,7 +94,10 @@ def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor) -> 
             # T-contiguous operands: both transposed by the HIP kernel (~5 TB/s) into scratch, then
             # the TN GEMM (1.30-1.44 vs 1.06-1.16 PF/s on the NT layout, profiles/r2_gemm_layouts)
             T, N, K = go2.shape[0], go2.shape[1], x2.shape[1]
-            gt = transpose(go2, out=_wgrad_scratch(N * T, go2.dtype, go2.device, "gt").view(N, T))
+            if go_t is not None and go_t.shape == (N, T) and go_t.is_contiguous() and go_t.dtype == go2.dtype:
+                gt = go_t
+            else:
+                gt = transpose(go2, out=_wgrad_scratch(N * T, go2.dtype, go2.device, "gt").view(N, T))
             xt = transpose(x2, out=_wgrad_scratch(K * T, x2.dtype, x2.device, "xt").view(K, T))
             ext().gemm(gt, xt.t(), mg, None, 1.0, 1.0)
             return

@@ -85,12 +85,13 @@ def _notify(param):
         cb(param)
 
 
-def _accumulate_wgrad(weight: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor):
-    """dW = go2^T @ x2; accumulated into weight.main_grad (fp32) if present, else returned."""
+def _accumulate_wgrad(weight: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor, go_t: torch.Tensor = None):
+    """dW = go2^T @ x2; accumulated into weight.main_grad (fp32) if present, else returned.
+    `go_t` is an optional producer-written transpose of go2 (see ops/activations.py)."""
     mg = getattr(weight, "main_grad", None)
     if mg is None:
         return go2.t().matmul(x2)
-    _gemm.wgrad_accumulate_(mg, go2, x2)
+    _gemm.wgrad_accumulate_(mg, go2, x2, go_t=go_t)
     _notify(weight)
     return None
 
@@ -141,6 +142,7 @@ class LinearWithAsyncCommunication(torch.autograd.Function):
             total_input = sp.sp_gather(inp, ctx.process_group)
         else:
             total_input = inp
+        go_t = getattr(grad_output, "_nxd_t", None)   # token-contiguous copy from the SwiGLU backward
         grad_output = grad_output.contiguous()
         group = ctx.process_group if ctx.process_group is not None else get_tensor_model_parallel_group()
         handles = []
@@ -152,7 +154,7 @@ class LinearWithAsyncCommunication(torch.autograd.Function):
                 handles = [dist.all_reduce(grad_input, group=group, async_op=True)]
         go2 = grad_output.reshape(-1, grad_output.shape[-1])
         x2 = total_input.reshape(-1, total_input.shape[-1])
-        grad_weight = _accumulate_wgrad(weight, go2, x2) if ctx.needs_input_grad[1] else None
+        grad_weight = _accumulate_wgrad(weight, go2, x2, go_t=go_t) if ctx.needs_input_grad[1] else None
         grad_bias = _bias_grad(bias, go2) if ctx.use_bias else None
         for h in handles:
             h.wait()

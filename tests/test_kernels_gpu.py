@@ -182,6 +182,58 @@ def test_swiglu():
     assert _rel(gu.grad, gf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("rows,I", [(128, 1792), (8192, 1792), (192, 448)])
+def test_swiglu_bwd_dual_layout(rows, I):
+    """Dual-layout SwiGLU backward: the row-major d(gate_up) matches the plain kernel bit for bit
+    and vs fp32, and the second output is exactly its transpose."""
+    C = _ext.ext()
+    gu = torch.randn(rows, 2 * I, device=DEV, dtype=torch.bfloat16)
+    dh = torch.randn(rows, I, device=DEV, dtype=torch.bfloat16)
+    ref = torch.empty_like(gu)
+    C.swiglu_bwd(gu, dh, ref)
+    dgu = torch.empty_like(gu)
+    dgu_t = torch.full((2 * I, rows), float("nan"), device=DEV, dtype=torch.bfloat16)
+    C.swiglu_bwd_dual(gu, dh, dgu, dgu_t)
+    torch.cuda.synchronize()
+    assert torch.equal(dgu, ref)
+    assert torch.equal(dgu_t, dgu.t())
+    gf = gu.float().requires_grad_(True)
+    ops.swiglu_reference(gf).backward(dh.float())
+    assert _rel(dgu, gf.grad) < 2e-2
+
+
+def test_swiglu_transposed_grad_reaches_gate_up_wgrad(monkeypatch):
+    """The SwiGLU backward's token-contiguous d(gate_up) is what the gate_up weight gradient
+    consumes (no separate transpose), with the same fp32 main_grad as the transposing path."""
+    from neuronx_distributed_llama3_2_amd.ops import activations, gemm
+    from neuronx_distributed_llama3_2_amd.parallel_layers import layers
+
+    monkeypatch.setattr(gemm, "_WGRAD_T", "2")   # TN layout at this small size too
+    seen = []
+    orig = gemm.wgrad_accumulate_
+
+    def spy(mg, go2, x2, go_t=None):
+        seen.append(go_t is not None)
+        return orig(mg, go2, x2, go_t=go_t)
+
+    monkeypatch.setattr(gemm, "wgrad_accumulate_", spy)
+    torch.manual_seed(0)
+    T, H, I = 256, 512, 1024
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    w = (0.05 * torch.randn(2 * I, H, device=DEV)).to(torch.bfloat16)
+    dh = torch.randn(T, I, device=DEV, dtype=torch.bfloat16)
+    grads = []
+    for dual in (True, False):
+        monkeypatch.setattr(activations, "_DUAL", dual)
+        wp = torch.nn.Parameter(w.clone())
+        wp.main_grad = torch.zeros(2 * I, H, device=DEV, dtype=torch.float32)
+        gu = layers.LinearWithAsyncCommunication.apply(x, wp, None, False, False, True, object())  # no TP group
+        ops.swiglu(gu).backward(dh)
+        grads.append(wp.main_grad.clone())
+    assert seen == [True, False], seen
+    assert torch.equal(grads[0], grads[1])
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("smooth", [0.0, 0.1])
 def test_cross_entropy(dtype, smooth):
