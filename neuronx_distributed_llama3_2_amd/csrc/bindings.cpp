@@ -26,6 +26,7 @@ int rope_inplace_launch(void*, int64_t, int64_t, int, int, int, const float*, co
 int swiglu_fwd_launch(const void*, void*, int64_t, int, hipStream_t);
 int swiglu_bwd_launch(const void*, const void*, void*, int64_t, int, hipStream_t);
 int swiglu_bwd_dual_launch(const void*, const void*, void*, void*, int64_t, int, hipStream_t);
+int swiglu_fwd_dual_launch(const void*, void*, void*, int64_t, int, hipStream_t);
 int xent_stats_launch(const void*, int, const int64_t*, float*, int64_t, int, int64_t, int64_t, hipStream_t);
 int xent_bwd_launch(const void*, int, const int64_t*, const float*, void*, int64_t, int, int64_t, int64_t, int64_t, float,
                     int64_t, hipStream_t);
@@ -254,6 +255,22 @@ void swiglu_bwd(at::Tensor gu, at::Tensor dh, at::Tensor dgu) {
   TORCH_CHECK(dh.numel() * 2 == gu.numel() && dgu.numel() == gu.numel(), "shape mismatch");
   check_rc(nxd::swiglu_bwd_launch(gu.data_ptr(), dh.data_ptr(), dgu.data_ptr(), gu.numel() / I2, (int)(I2 / 2), cur_stream()),
            "swiglu_bwd");
+}
+
+// h = silu(g) * u and its transpose h_t [I, rows] (contiguous); rows and I multiples of 64.
+void swiglu_fwd_dual(at::Tensor gu, at::Tensor h, at::Tensor h_t) {
+  const int64_t I2 = gu.size(-1);
+  rows_check(gu, "gate_up", I2);
+  rows_check(h, "h", I2 / 2);
+  TORCH_CHECK(h.numel() * 2 == gu.numel(), "shape mismatch");
+  const int64_t N = gu.numel() / I2;
+  check_bf16(h_t, "h_t");
+  TORCH_CHECK(h_t.dim() == 2 && h_t.size(0) == I2 / 2 && h_t.size(1) == N && h_t.is_contiguous(),
+              "h_t must be contiguous [I, rows]");
+  TORCH_CHECK(N % 64 == 0 && (I2 / 2) % 64 == 0, "swiglu_fwd_dual: rows and I must be multiples of 64");
+  check_aligned16(h_t, "h_t");
+  check_rc(nxd::swiglu_fwd_dual_launch(gu.data_ptr(), h.data_ptr(), h_t.data_ptr(), N, (int)(I2 / 2), cur_stream()),
+           "swiglu_fwd_dual");
 }
 
 // dgu and its transpose dgu_t [2I, rows] (contiguous) in one kernel; rows and I multiples of 64.
@@ -829,6 +846,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("transpose_bf16", &transpose_bf16);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("swiglu_bwd_dual", &swiglu_bwd_dual);
+  m.def("swiglu_fwd_dual", &swiglu_fwd_dual);
   m.def("xent_stats", &xent_stats);
   m.def("xent_bwd", &xent_bwd);
   m.def("flat_reduce", &flat_reduce);

@@ -57,19 +57,22 @@ __global__ void __launch_bounds__(256) bwd_kernel(const uint16_t* __restrict__ g
 // workgroup owns a 64-row x 64-column tile of the gate and up halves: the row-major result is
 // written straight from registers, the transposed one goes through LDS and leaves as 16-byte
 // vectors of 8 consecutive rows (tokens).  N % 64 == 0 and I % 64 == 0 (checked by the launcher).
-constexpr int TT = 64;
+constexpr int TT = 64;         // tile columns (of each half)
 constexpr int LDT = TT + 8;   // LDS row stride (elements): 16-B aligned rows, offset banks
 
+// TR = tile rows (tokens): 128 gives 256-B contiguous runs per transposed row, 64 covers N % 128 != 0
+template <int TR>
 __global__ void __launch_bounds__(256) bwd_dual_kernel(const uint16_t* __restrict__ gu, const uint16_t* __restrict__ dh,
                                                        uint16_t* __restrict__ dgu, uint16_t* __restrict__ dgu_t, int64_t N,
                                                        int I) {
-  __shared__ __attribute__((aligned(16))) uint16_t sdg[TT * LDT];
-  __shared__ __attribute__((aligned(16))) uint16_t sdu[TT * LDT];
+  __shared__ __attribute__((aligned(16))) uint16_t sdg[TR * LDT];
+  __shared__ __attribute__((aligned(16))) uint16_t sdu[TR * LDT];
+  constexpr int NV = TR * TT / 8 / 256;   // 16-B vectors per thread per phase
   const int tid = threadIdx.x;
   const int col0 = blockIdx.x * TT;
-  const int64_t row0 = (int64_t)blockIdx.y * TT;
+  const int64_t row0 = (int64_t)blockIdx.y * TR;
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
+  for (int it = 0; it < NV; ++it) {
     const int v = tid + 256 * it, r = v >> 3, c = (v & 7) * 8;
     const int64_t row = row0 + r;
     const uint16_t* src = gu + row * 2 * I + col0 + c;
@@ -91,9 +94,10 @@ __global__ void __launch_bounds__(256) bwd_dual_kernel(const uint16_t* __restric
     *reinterpret_cast<u32x4_t*>(sdu + r * LDT + c) = pu;
   }
   __syncthreads();
+  constexpr int RV = TR / 8;   // 8-token vectors per transposed row
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int v = tid + 256 * it, c = v >> 3, r = (v & 7) * 8;   // column c, tokens r .. r + 7
+  for (int it = 0; it < NV; ++it) {
+    const int v = tid + 256 * it, c = v / RV, r = (v % RV) * 8;   // column c, tokens r .. r + 7
     uint32_t wg[4], wu[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -102,6 +106,43 @@ __global__ void __launch_bounds__(256) bwd_dual_kernel(const uint16_t* __restric
     }
     *reinterpret_cast<u32x4_t*>(dgu_t + (int64_t)(col0 + c) * N + row0 + r) = u32x4_t{wg[0], wg[1], wg[2], wg[3]};
     *reinterpret_cast<u32x4_t*>(dgu_t + (int64_t)(I + col0 + c) * N + row0 + r) = u32x4_t{wu[0], wu[1], wu[2], wu[3]};
+  }
+}
+
+// Forward with a second, transposed copy of h ([I, N], token-contiguous): the down projection's
+// weight gradient (TN GEMM) reads it instead of transposing the saved activation in backward.
+template <int TR>
+__global__ void __launch_bounds__(256) fwd_dual_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ h,
+                                                       uint16_t* __restrict__ h_t, int64_t N, int I) {
+  __shared__ __attribute__((aligned(16))) uint16_t sh[TR * LDT];
+  constexpr int NV = TR * TT / 8 / 256;
+  const int tid = threadIdx.x;
+  const int col0 = blockIdx.x * TT;
+  const int64_t row0 = (int64_t)blockIdx.y * TR;
+#pragma unroll
+  for (int it = 0; it < NV; ++it) {
+    const int v = tid + 256 * it, r = v >> 3, c = (v & 7) * 8;
+    const int64_t row = row0 + r;
+    const uint16_t* src = gu + row * 2 * I + col0 + c;
+    float g[8], u[8], o[8];
+    unpack8(*reinterpret_cast<const u32x4_t*>(src), g);
+    unpack8(*reinterpret_cast<const u32x4_t*>(src + I), u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = g[j] * sigm(g[j]) * u[j];
+    const u32x4_t po = pack8(o);
+    *reinterpret_cast<u32x4_t*>(h + row * I + col0 + c) = po;
+    *reinterpret_cast<u32x4_t*>(sh + r * LDT + c) = po;
+  }
+  __syncthreads();
+  constexpr int RV = TR / 8;
+#pragma unroll
+  for (int it = 0; it < NV; ++it) {
+    const int v = tid + 256 * it, c = v / RV, r = (v % RV) * 8;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = (uint32_t)sh[(r + 2 * j) * LDT + c] | ((uint32_t)sh[(r + 2 * j + 1) * LDT + c] << 16);
+    *reinterpret_cast<u32x4_t*>(h_t + (int64_t)(col0 + c) * N + row0 + r) = u32x4_t{w[0], w[1], w[2], w[3]};
   }
 }
 
@@ -130,13 +171,35 @@ int swiglu_bwd_launch(const void* gu, const void* dh, void* dgu, int64_t N, int 
   return (int)hipGetLastError();
 }
 
+// h [N, I] and h_t [I, N] in one pass; -1 if the shape is not tiled.
+int swiglu_fwd_dual_launch(const void* gu, void* h, void* h_t, int64_t N, int I, hipStream_t stream) {
+  if (I % swiglu::TT || N % 64 || N / 64 > 65535) return -1;
+  if (N == 0) return 0;
+  const bool big = N % 128 == 0;
+  const dim3 grid((unsigned)(I / swiglu::TT), (unsigned)(N / (big ? 128 : 64)));
+  if (big)
+    hipLaunchKernelGGL(swiglu::fwd_dual_kernel<128>, grid, dim3(256), 0, stream, (const uint16_t*)gu, (uint16_t*)h,
+                       (uint16_t*)h_t, N, I);
+  else
+    hipLaunchKernelGGL(swiglu::fwd_dual_kernel<64>, grid, dim3(256), 0, stream, (const uint16_t*)gu, (uint16_t*)h,
+                       (uint16_t*)h_t, N, I);
+  return (int)hipGetLastError();
+}
+
 // dgu [N, 2I] row-major and dgu_t [2I, N] (its transpose) in one pass; -1 if the shape is not tiled.
 int swiglu_bwd_dual_launch(const void* gu, const void* dh, void* dgu, void* dgu_t, int64_t N, int I, hipStream_t stream) {
-  if (I % swiglu::TT || N % swiglu::TT || N / swiglu::TT > 65535) return -1;
+  if (I % swiglu::TT || N % 64 || N / 64 > 65535) return -1;
   if (N == 0) return 0;
-  const dim3 grid((unsigned)(I / swiglu::TT), (unsigned)(N / swiglu::TT));
-  hipLaunchKernelGGL(swiglu::bwd_dual_kernel, grid, dim3(256), 0, stream, (const uint16_t*)gu, (const uint16_t*)dh,
-                     (uint16_t*)dgu, (uint16_t*)dgu_t, N, I);
+  // NXD_SWIGLU_DUAL_ROWS=64 forces the 64-row tile (A/B); read once
+  static const int rows_knob = [] { const char* e = getenv("NXD_SWIGLU_DUAL_ROWS"); return e ? atoi(e) : 128; }();
+  const bool big = rows_knob == 128 && N % 128 == 0;
+  const dim3 grid((unsigned)(I / swiglu::TT), (unsigned)(N / (big ? 128 : 64)));
+  if (big)
+    hipLaunchKernelGGL(swiglu::bwd_dual_kernel<128>, grid, dim3(256), 0, stream, (const uint16_t*)gu, (const uint16_t*)dh,
+                       (uint16_t*)dgu, (uint16_t*)dgu_t, N, I);
+  else
+    hipLaunchKernelGGL(swiglu::bwd_dual_kernel<64>, grid, dim3(256), 0, stream, (const uint16_t*)gu, (const uint16_t*)dh,
+                       (uint16_t*)dgu, (uint16_t*)dgu_t, N, I);
   return (int)hipGetLastError();
 }
 

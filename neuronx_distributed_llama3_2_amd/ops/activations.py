@@ -3,7 +3,9 @@
 The backward also writes d(gate_up) transposed ([2I, T], token-contiguous) when the shape tiles by
 64: the gate_up weight gradient runs as a TN GEMM on T-contiguous operands (ops/gemm.py), and the
 transposed copy — attached to the returned gradient as `_nxd_t` — replaces the separate transpose
-of the layer's largest activation gradient.  NXD_SWIGLU_DUAL=0 disables it.
+of the layer's largest activation gradient.  NXD_SWIGLU_DUAL=0 disables it.  Likewise the forward
+(under autograd) writes h transposed, `h._nxd_t`, which the down projection saves in place of h for
+its TN weight gradient (NXD_SWIGLU_DUAL_FWD=0 disables).
 """
 
 from __future__ import annotations
@@ -22,14 +24,24 @@ def swiglu_reference(gu: torch.Tensor) -> torch.Tensor:
 
 
 _DUAL = os.environ.get("NXD_SWIGLU_DUAL", "1") == "1"
+_DUAL_FWD = os.environ.get("NXD_SWIGLU_DUAL_FWD", "0") == "1"
 
 
 class SwiGLUFunc(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gu):
+    def forward(ctx, gu, want_t=False):
         gu = gu.contiguous()
         h = torch.empty(gu.shape[:-1] + (gu.shape[-1] // 2,), dtype=gu.dtype, device=gu.device)
-        ext().swiglu_fwd(gu, h)
+        I = h.shape[-1]
+        rows = h.numel() // I if I else 0
+        if want_t and rows and rows % 64 == 0 and I % 64 == 0:
+            # token-contiguous copy of h for the down projection's weight gradient (saved by the
+            # next linear instead of h itself, see parallel_layers/layers.py)
+            h_t = torch.empty((I, rows), dtype=gu.dtype, device=gu.device)
+            ext().swiglu_fwd_dual(gu, h, h_t)
+            h._nxd_t = h_t
+        else:
+            ext().swiglu_fwd(gu, h)
         ctx.save_for_backward(gu)
         return h
 
@@ -43,13 +55,13 @@ class SwiGLUFunc(torch.autograd.Function):
             dgu_t = torch.empty((I2, rows), dtype=gu.dtype, device=gu.device)
             ext().swiglu_bwd_dual(gu, dh.contiguous(), dgu, dgu_t)
             dgu._nxd_t = dgu_t
-            return dgu
+            return dgu, None
         ext().swiglu_bwd(gu, dh.contiguous(), dgu)
-        return dgu
+        return dgu, None
 
 
 def swiglu(gu: torch.Tensor) -> torch.Tensor:
     """h = silu(gate) * up for gu = [gate | up] along the last dim."""
     if use_native(gu):
-        return SwiGLUFunc.apply(gu)
+        return SwiGLUFunc.apply(gu, _DUAL_FWD and torch.is_grad_enabled() and gu.requires_grad)
     return swiglu_reference(gu)

@@ -62,11 +62,16 @@ _scratch = {}
 _WGRAD_T = os.environ.get("NXD_WGRAD_T", "1")
 
 
-def _use_wgrad_t(go2: torch.Tensor, x2: torch.Tensor) -> bool:
+def _use_wgrad_t(go2: torch.Tensor, x2: torch.Tensor = None, K: int = None) -> bool:
+    """TN layout for this wgrad?  x2 = None: the caller holds a contiguous token-major copy of x
+    with K rows (only go2's strides matter)."""
     if _WGRAD_T == "0" or _WGRAD_BF16:
         return False
-    T, N, K = go2.shape[0], go2.shape[1], x2.shape[1]
-    if T % 8 or N % 8 or K % 8 or go2.stride(-1) != 1 or x2.stride(-1) != 1 or go2.stride(0) % 8 or x2.stride(0) % 8:
+    T, N = go2.shape[0], go2.shape[1]
+    K = x2.shape[1] if x2 is not None else K
+    if T % 8 or N % 8 or K % 8 or go2.stride(-1) != 1 or go2.stride(0) % 8:
+        return False
+    if x2 is not None and (x2.stride(-1) != 1 or x2.stride(0) % 8):
         return False
     return _WGRAD_T == "2" or N * K / (N + K) > 1200
 
@@ -79,26 +84,35 @@ def _wgrad_scratch(n: int, dtype, device, tag: str = "") -> torch.Tensor:
     return t[:n]
 
 
-def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor, go_t: torch.Tensor = None) -> None:
+def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2, go_t: torch.Tensor = None,
+                      x_t: torch.Tensor = None) -> None:
     """mg [N, K] (fp32) += go2[T, N]^T @ x2[T, K].
 
-    `go_t`: optional contiguous [N, T] copy of go2 already written by its producer (the SwiGLU
-    backward), used instead of transposing go2 when the TN layout is taken.
+    `go_t` / `x_t`: optional contiguous [N, T] / [K, T] copies of go2 / x2 already written by their
+    producers (the SwiGLU backward / forward), used instead of transposing when the TN layout is
+    taken.  x2 may be None when only x_t was kept.
 
     Default: one hipBLASLt GEMM with fp32 C/D and beta = 1.  NXD_WGRAD_BF16=1: bf16-output GEMM
     into a reused scratch, then an fp32 add (the per-micro-batch weight gradient is rounded to
     bf16 before the fp32 accumulation — the precision of the reference's XLA matmul + fp32
     grad accumulation; hipBLASLt's bf16-output solutions run faster than its fp32-output ones)."""
-    if _native(go2, x2) and mg.is_contiguous():
-        if _use_wgrad_t(go2, x2):
+    if x_t is not None and not (x_t.dim() == 2 and x_t.is_contiguous() and x_t.shape[1] == go2.shape[0]):
+        x_t = None
+    if x2 is None and not (x_t is not None and _native(go2, x_t) and mg.is_contiguous()
+                           and _use_wgrad_t(go2, K=x_t.shape[0])):
+        x2 = x_t.t().contiguous()   # only the token-major copy was kept and the TN path is off
+        x_t = None
+    if x2 is None or (_native(go2, x2) and mg.is_contiguous()):
+        if x2 is None or _use_wgrad_t(go2, x2):
             # T-contiguous operands: both transposed by the HIP kernel (~5 TB/s) into scratch, then
             # the TN GEMM (1.30-1.44 vs 1.06-1.16 PF/s on the NT layout, profiles/r2_gemm_layouts)
-            T, N, K = go2.shape[0], go2.shape[1], x2.shape[1]
+            T, N = go2.shape[0], go2.shape[1]
+            K = x_t.shape[0] if x_t is not None else x2.shape[1]
             if go_t is not None and go_t.shape == (N, T) and go_t.is_contiguous() and go_t.dtype == go2.dtype:
                 gt = go_t
             else:
                 gt = transpose(go2, out=_wgrad_scratch(N * T, go2.dtype, go2.device, "gt").view(N, T))
-            xt = transpose(x2, out=_wgrad_scratch(K * T, x2.dtype, x2.device, "xt").view(K, T))
+            xt = x_t if x_t is not None else transpose(x2, out=_wgrad_scratch(K * T, x2.dtype, x2.device, "xt").view(K, T))
             ext().gemm(gt, xt.t(), mg, None, 1.0, 1.0)
             return
         if _WGRAD_BF16:

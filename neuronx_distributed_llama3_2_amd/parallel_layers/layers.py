@@ -85,15 +85,26 @@ def _notify(param):
         cb(param)
 
 
-def _accumulate_wgrad(weight: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor, go_t: torch.Tensor = None):
+def _accumulate_wgrad(weight: torch.Tensor, go2: torch.Tensor, x2, go_t: torch.Tensor = None,
+                      x_t: torch.Tensor = None):
     """dW = go2^T @ x2; accumulated into weight.main_grad (fp32) if present, else returned.
-    `go_t` is an optional producer-written transpose of go2 (see ops/activations.py)."""
+    `go_t` / `x_t` are optional producer-written transposes of go2 / x2 (see ops/activations.py);
+    x2 may be None when only x_t was saved."""
     mg = getattr(weight, "main_grad", None)
     if mg is None:
-        return go2.t().matmul(x2)
-    _gemm.wgrad_accumulate_(mg, go2, x2, go_t=go_t)
+        return go2.t().matmul(x2 if x2 is not None else x_t.t())
+    _gemm.wgrad_accumulate_(mg, go2, x2, go_t=go_t, x_t=x_t)
     _notify(weight)
     return None
+
+
+def _token_major_copy(x: torch.Tensor):
+    """The producer-written [K, tokens] copy of activation x ([..., K]) if one is attached."""
+    t = getattr(x, "_nxd_t", None)
+    if t is None or t.dim() != 2 or not t.is_contiguous() or x.dim() < 1:
+        return None
+    K = x.shape[-1]
+    return t if t.shape == (K, x.numel() // max(K, 1)) else None
 
 
 def _bias_grad(bias, go2):
@@ -128,9 +139,16 @@ class LinearWithAsyncCommunication(torch.autograd.Function):
             total_input = input
             output = _gemm.linear(total_input, weight)
         ctx.saved_gathered = sequence_parallel_enabled and _SAVE_GATHERED_INPUT
+        # a token-major copy of the input written by its producer (SwiGLU forward) is saved
+        # INSTEAD of the input: the weight gradient is the only backward use of it
+        x_t = _token_major_copy(input) if not sequence_parallel_enabled else None
+        ctx.x_is_t = x_t is not None
         if save_for_backward:
-            ctx.save_for_backward(total_input if (ctx.saved_gathered or not sequence_parallel_enabled) else input, weight,
-                                  bias)
+            if ctx.x_is_t:
+                ctx.save_for_backward(x_t, weight, bias)
+            else:
+                ctx.save_for_backward(total_input if (ctx.saved_gathered or not sequence_parallel_enabled) else input,
+                                      weight, bias)
         if bias is not None:
             output = output + bias
         return output
@@ -138,7 +156,10 @@ class LinearWithAsyncCommunication(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_output):
         inp, weight, bias = ctx.saved_tensors
-        if ctx.sequence_parallel_enabled and not ctx.saved_gathered:
+        x_t = None
+        if ctx.x_is_t:
+            x_t, total_input = inp, None
+        elif ctx.sequence_parallel_enabled and not ctx.saved_gathered:
             total_input = sp.sp_gather(inp, ctx.process_group)
         else:
             total_input = inp
@@ -153,8 +174,8 @@ class LinearWithAsyncCommunication(torch.autograd.Function):
             if not ctx.sequence_parallel_enabled and ctx.async_grad_allreduce and dist.get_world_size(group=group) > 1:
                 handles = [dist.all_reduce(grad_input, group=group, async_op=True)]
         go2 = grad_output.reshape(-1, grad_output.shape[-1])
-        x2 = total_input.reshape(-1, total_input.shape[-1])
-        grad_weight = _accumulate_wgrad(weight, go2, x2, go_t=go_t) if ctx.needs_input_grad[1] else None
+        x2 = total_input.reshape(-1, total_input.shape[-1]) if total_input is not None else None
+        grad_weight = _accumulate_wgrad(weight, go2, x2, go_t=go_t, x_t=x_t) if ctx.needs_input_grad[1] else None
         grad_bias = _bias_grad(bias, go2) if ctx.use_bias else None
         for h in handles:
             h.wait()
@@ -170,7 +191,9 @@ class RowParallelSPLinear(torch.autograd.Function):
     def forward(ctx, input, weight, process_group=None):
         ctx.process_group = process_group
         local, hs = sp.linear_reduce_scatter_start(input, weight, process_group)
-        ctx.save_for_backward(input, weight)
+        x_t = _token_major_copy(input)
+        ctx.x_is_t = x_t is not None
+        ctx.save_for_backward(x_t if ctx.x_is_t else input, weight)
         for h in hs:
             h.wait()
         return local
@@ -180,8 +203,9 @@ class RowParallelSPLinear(torch.autograd.Function):
         inp, weight = ctx.saved_tensors
         grad_input, g_full = sp.gather_matmul(grad_output.contiguous(), weight, ctx.process_group)
         go2 = g_full.reshape(-1, g_full.shape[-1])
-        x2 = inp.reshape(-1, inp.shape[-1])
-        grad_weight = _accumulate_wgrad(weight, go2, x2) if ctx.needs_input_grad[1] else None
+        x_t = inp if ctx.x_is_t else None
+        x2 = None if ctx.x_is_t else inp.reshape(-1, inp.shape[-1])
+        grad_weight = _accumulate_wgrad(weight, go2, x2, x_t=x_t) if ctx.needs_input_grad[1] else None
         return grad_input, grad_weight, None
 
 

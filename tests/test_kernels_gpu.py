@@ -212,9 +212,9 @@ def test_swiglu_transposed_grad_reaches_gate_up_wgrad(monkeypatch):
     seen = []
     orig = gemm.wgrad_accumulate_
 
-    def spy(mg, go2, x2, go_t=None):
+    def spy(mg, go2, x2, go_t=None, x_t=None):
         seen.append(go_t is not None)
-        return orig(mg, go2, x2, go_t=go_t)
+        return orig(mg, go2, x2, go_t=go_t, x_t=x_t)
 
     monkeypatch.setattr(gemm, "wgrad_accumulate_", spy)
     torch.manual_seed(0)
@@ -232,6 +232,48 @@ def test_swiglu_transposed_grad_reaches_gate_up_wgrad(monkeypatch):
         grads.append(wp.main_grad.clone())
     assert seen == [True, False], seen
     assert torch.equal(grads[0], grads[1])
+
+
+def test_swiglu_forward_token_major_copy_feeds_down_wgrad(monkeypatch):
+    """SwiGLU forward under autograd writes h token-major; the down projection saves that copy
+    instead of h and its weight gradient equals the transposing path's bit for bit."""
+    from neuronx_distributed_llama3_2_amd.ops import activations, gemm
+    from neuronx_distributed_llama3_2_amd.parallel_layers import layers
+
+    monkeypatch.setattr(gemm, "_WGRAD_T", "2")
+    C = _ext.ext()
+    gu0 = torch.randn(2, 192, 2 * 448, device=DEV, dtype=torch.bfloat16)
+    h_ref = torch.empty(2, 192, 448, device=DEV, dtype=torch.bfloat16)
+    h_t = torch.empty(448, 384, device=DEV, dtype=torch.bfloat16)
+    C.swiglu_fwd_dual(gu0, h_ref, h_t)
+    torch.cuda.synchronize()
+    assert torch.equal(h_t, h_ref.reshape(-1, 448).t())
+    assert _rel(h_ref, ops.swiglu_reference(gu0.float())) < 1e-2
+    seen = []
+    orig = gemm.wgrad_accumulate_
+
+    def spy(mg, go2, x2, go_t=None, x_t=None):
+        seen.append((x2 is None, x_t is not None))
+        return orig(mg, go2, x2, go_t=go_t, x_t=x_t)
+
+    monkeypatch.setattr(gemm, "wgrad_accumulate_", spy)
+    w = (0.05 * torch.randn(256, 448, device=DEV)).to(torch.bfloat16)
+    dy = torch.randn(2, 192, 256, device=DEV, dtype=torch.bfloat16)
+    grads, outs = [], []
+    for dual in (True, False):
+        monkeypatch.setattr(activations, "_DUAL_FWD", dual)
+        gu = gu0.clone().requires_grad_(True)
+        wp = torch.nn.Parameter(w.clone())
+        wp.main_grad = torch.zeros(256, 448, device=DEV, dtype=torch.float32)
+        h = ops.swiglu(gu)
+        assert hasattr(h, "_nxd_t") == dual
+        y = layers.LinearWithAsyncCommunication.apply(h, wp, None, False, False, True, object())
+        y.backward(dy)
+        outs.append((y.detach().clone(), gu.grad.clone()))
+        grads.append(wp.main_grad.clone())
+    assert seen == [(True, True), (False, False)], seen
+    assert torch.equal(grads[0], grads[1])
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
