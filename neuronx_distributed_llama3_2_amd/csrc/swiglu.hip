@@ -175,7 +175,8 @@ int swiglu_bwd_launch(const void* gu, const void* dh, void* dgu, int64_t N, int 
 int swiglu_fwd_dual_launch(const void* gu, void* h, void* h_t, int64_t N, int I, hipStream_t stream) {
   if (I % swiglu::TT || N % 64 || N / 64 > 65535) return -1;
   if (N == 0) return 0;
-  const bool big = N % 128 == 0;
+  static const int rows_knob = [] { const char* e = getenv("NXD_SWIGLU_DUAL_ROWS"); return e ? atoi(e) : 64; }();
+  const bool big = rows_knob == 128 && N % 128 == 0;
   const dim3 grid((unsigned)(I / swiglu::TT), (unsigned)(N / (big ? 128 : 64)));
   if (big)
     hipLaunchKernelGGL(swiglu::fwd_dual_kernel<128>, grid, dim3(256), 0, stream, (const uint16_t*)gu, (uint16_t*)h,
@@ -190,8 +191,9 @@ int swiglu_fwd_dual_launch(const void* gu, void* h, void* h_t, int64_t N, int I,
 int swiglu_bwd_dual_launch(const void* gu, const void* dh, void* dgu, void* dgu_t, int64_t N, int I, hipStream_t stream) {
   if (I % swiglu::TT || N % 64 || N / 64 > 65535) return -1;
   if (N == 0) return 0;
-  // NXD_SWIGLU_DUAL_ROWS=64 forces the 64-row tile (A/B); read once
-  static const int rows_knob = [] { const char* e = getenv("NXD_SWIGLU_DUAL_ROWS"); return e ? atoi(e) : 128; }();
+  // 64-row tiles measured faster than 128 (379 vs 387-397 us at T=8192, I=14336; 34.6 vs 39.5 at the
+  // TP=8 shard, profiles/r2_swiglu_dual_kernel_ab.jsonl); NXD_SWIGLU_DUAL_ROWS=128 selects the other; read once
+  static const int rows_knob = [] { const char* e = getenv("NXD_SWIGLU_DUAL_ROWS"); return e ? atoi(e) : 64; }();
   const bool big = rows_knob == 128 && N % 128 == 0;
   const dim3 grid((unsigned)(I / swiglu::TT), (unsigned)(N / (big ? 128 : 64)));
   if (big)

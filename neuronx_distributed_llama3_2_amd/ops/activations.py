@@ -24,7 +24,7 @@ def swiglu_reference(gu: torch.Tensor) -> torch.Tensor:
 
 
 _DUAL = os.environ.get("NXD_SWIGLU_DUAL", "1") == "1"
-_DUAL_FWD = os.environ.get("NXD_SWIGLU_DUAL_FWD", "0") == "1"
+_DUAL_FWD = os.environ.get("NXD_SWIGLU_DUAL_FWD", "1") == "1"
 
 
 class SwiGLUFunc(torch.autograd.Function):
