@@ -34,11 +34,18 @@ def main():
         dual = _time(lambda: C.swiglu_bwd_dual(gu, dh, dgu, dgu_t))
         plain = _time(lambda: C.swiglu_bwd(gu, dh, dgu))
         tr = _time(lambda: C.transpose_bf16(dgu, dgu_t))
+        h = torch.empty_like(dh)
+        h_t = torch.empty(I, T, device="cuda", dtype=torch.bfloat16)
+        fdual = _time(lambda: C.swiglu_fwd_dual(gu, h, h_t))
+        fplain = _time(lambda: C.swiglu_fwd(gu, h))
+        ftr = _time(lambda: C.transpose_bf16(h, h_t))
         gb = (gu.numel() + dh.numel() + 2 * dgu.numel()) * 2 / 1e9
         print(json.dumps({"T": T, "I": I, "rows_tile": int(os.environ.get("NXD_SWIGLU_DUAL_ROWS", "128")),
                           "dual_us": round(dual, 1), "dual_TBps": round(gb / dual * 1e6 / 1e3, 2),
                           "plain_bwd_us": round(plain, 1), "transpose_us": round(tr, 1),
-                          "saved_us": round(plain + tr - dual, 1)}), flush=True)
+                          "saved_us": round(plain + tr - dual, 1), "fwd_dual_us": round(fdual, 1),
+                          "fwd_plain_us": round(fplain, 1), "fwd_transpose_us": round(ftr, 1),
+                          "fwd_saved_us": round(fplain + ftr - fdual, 1)}), flush=True)
 
 
 if __name__ == "__main__":
