@@ -73,9 +73,9 @@ class LlamaMLP(nn.Module):
     def forward(self, x):
         gu = self.gate_up_proj(x)
         if self.selective_checkpoint and self.training:
-            h = checkpoint(ops.swiglu, gu, use_reentrant=False)
+            h = checkpoint(ops.swiglu, gu, True, use_reentrant=False)
         else:
-            h = ops.swiglu(gu)
+            h = ops.swiglu(gu, token_major=True)   # token-major copies feed the TN weight gradients
         return self.down_proj(h)
 
 

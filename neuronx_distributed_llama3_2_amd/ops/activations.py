@@ -29,8 +29,9 @@ _DUAL_FWD = os.environ.get("NXD_SWIGLU_DUAL_FWD", "1") == "1"
 
 class SwiGLUFunc(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gu, want_t=False):
+    def forward(ctx, gu, want_t=False, want_grad_t=False):
         gu = gu.contiguous()
+        ctx.want_grad_t = want_grad_t
         h = torch.empty(gu.shape[:-1] + (gu.shape[-1] // 2,), dtype=gu.dtype, device=gu.device)
         I = h.shape[-1]
         rows = h.numel() // I if I else 0
@@ -51,17 +52,22 @@ class SwiGLUFunc(torch.autograd.Function):
         dgu = torch.empty_like(gu)
         I2 = gu.shape[-1]
         rows = gu.numel() // I2 if I2 else 0
-        if _DUAL and rows and rows % 64 == 0 and (I2 // 2) % 64 == 0:
+        if ctx.want_grad_t and _DUAL and rows and rows % 64 == 0 and (I2 // 2) % 64 == 0:
             dgu_t = torch.empty((I2, rows), dtype=gu.dtype, device=gu.device)
             ext().swiglu_bwd_dual(gu, dh.contiguous(), dgu, dgu_t)
             dgu._nxd_t = dgu_t
-            return dgu, None
+            return dgu, None, None
         ext().swiglu_bwd(gu, dh.contiguous(), dgu)
-        return dgu, None
+        return dgu, None, None
 
 
-def swiglu(gu: torch.Tensor) -> torch.Tensor:
-    """h = silu(gate) * up for gu = [gate | up] along the last dim."""
+def swiglu(gu: torch.Tensor, token_major: bool = False) -> torch.Tensor:
+    """h = silu(gate) * up for gu = [gate | up] along the last dim.
+
+    token_major=True: the caller feeds gu from, and h into, the framework's linear layers (dense
+    MLP), which consume the token-major copies; other callers (MoE grouped GEMMs) would only pay
+    for them."""
     if use_native(gu):
-        return SwiGLUFunc.apply(gu, _DUAL_FWD and torch.is_grad_enabled() and gu.requires_grad)
+        train = token_major and torch.is_grad_enabled() and gu.requires_grad
+        return SwiGLUFunc.apply(gu, _DUAL_FWD and train, train)
     return swiglu_reference(gu)

@@ -228,7 +228,7 @@ def test_swiglu_transposed_grad_reaches_gate_up_wgrad(monkeypatch):
         wp = torch.nn.Parameter(w.clone())
         wp.main_grad = torch.zeros(2 * I, H, device=DEV, dtype=torch.float32)
         gu = layers.LinearWithAsyncCommunication.apply(x, wp, None, False, False, True, object())  # no TP group
-        ops.swiglu(gu).backward(dh)
+        ops.swiglu(gu, token_major=True).backward(dh)
         grads.append(wp.main_grad.clone())
     assert seen == [True, False], seen
     assert torch.equal(grads[0], grads[1])
@@ -265,7 +265,7 @@ def test_swiglu_forward_token_major_copy_feeds_down_wgrad(monkeypatch):
         gu = gu0.clone().requires_grad_(True)
         wp = torch.nn.Parameter(w.clone())
         wp.main_grad = torch.zeros(256, 448, device=DEV, dtype=torch.float32)
-        h = ops.swiglu(gu)
+        h = ops.swiglu(gu, token_major=True)
         assert hasattr(h, "_nxd_t") == dual
         y = layers.LinearWithAsyncCommunication.apply(h, wp, None, False, False, True, object())
         y.backward(dy)
