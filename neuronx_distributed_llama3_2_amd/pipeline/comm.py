@@ -32,37 +32,55 @@ class P2PGroup:
     def __init__(self):
         self.ops: List[dist.P2POp] = []
         self.keep: List[torch.Tensor] = []
+        # gloo (CPU tests, the one-GPU multi-rank rehearsal) moves raw pointers from its own host
+        # threads with no HIP stream ordering: GPU tensors are staged through host copies, a send
+        # after the producing stream finished, a receive copied in when its exchange is retired
+        self._stage = dist.is_initialized() and dist.get_backend() == "gloo"
+        self._copy_in: List[Tuple[torch.Tensor, torch.Tensor]] = []   # (host buffer, device tensor)
         self._inflight: List[Tuple[list, List[torch.Tensor]]] = []   # (works, tensors) per exchange
         self._exchange_of: dict = {}                                  # id(recv buffer) -> exchange
         self.max_inflight = 64   # bound on outstanding exchanges (oldest retired first)
 
     def send(self, t: torch.Tensor, dst: int):
         t = t.contiguous()
+        if self._stage and t.is_cuda:
+            t = t.detach().cpu()   # waits for the producing stream
         self.keep.append(t)
         self.ops.append(dist.P2POp(dist.isend, t, dst))
 
     def recv(self, t: torch.Tensor, src: int):
         self.keep.append(t)
-        self.ops.append(dist.P2POp(dist.irecv, t, src))
+        buf = t
+        if self._stage and t.is_cuda:
+            buf = torch.empty(t.shape, dtype=t.dtype, device="cpu")
+            self.keep.append(buf)
+            self._copy_in.append((buf, t))
+        self.ops.append(dist.P2POp(dist.irecv, buf, src))
 
     def issue(self) -> None:
         if not self.ops:
             return
         works = dist.batch_isend_irecv(self.ops)
-        ex = (list(works), self.keep)
+        ex = (list(works), self.keep, self._copy_in)
         self._inflight.append(ex)
         for op in self.ops:
             if op.op is dist.irecv:
                 self._exchange_of[id(op.tensor)] = ex
-        self.ops, self.keep = [], []
+        for _, dev in self._copy_in:
+            self._exchange_of[id(dev)] = ex
+        self.ops, self.keep, self._copy_in = [], [], []
         while len(self._inflight) > self.max_inflight:
             self._retire(self._inflight[0])
 
     def _retire(self, ex) -> None:
-        works, tensors = ex
+        works, tensors, copy_in = ex
         for w in works:
             w.wait()
         works.clear()
+        for host, dev in copy_in:
+            dev.copy_(host)
+            self._exchange_of.pop(id(dev), None)
+        copy_in.clear()
         for t in tensors:
             self._exchange_of.pop(id(t), None)
         if ex in self._inflight:
