@@ -12,7 +12,6 @@ int flash_attn_fwd_launch(const void*, const void*, const void*, void*, float*, 
 int64_t flash_attn_bwd_workspace(int, int, int, int, int, int);
 void flash_attn_bwd_set_knob(int, int);
 int transpose_bf16_launch(const void*, void*, int64_t, int64_t, int64_t, int64_t, hipStream_t);
-void flash_attn_fwd_set_variant(int);
 int flash_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*, float*,
                           void*, void*, void*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                           const int64_t*, const int64_t*, const int64_t*, const int64_t*, int, int, int, int, int, int,
@@ -834,11 +833,8 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "CDNA4 (gfx950) kernels of neuronx_distributed_llama3_2_amd";
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
-  // A/B knobs: 0 = bwd ablation flags, 1 = bwd chunk override (0 = auto), 2 = fwd variant bits
-  m.def("flash_attn_set_knob", [](int which, int value) {
-    if (which == 2) nxd::flash_attn_fwd_set_variant(value);
-    else nxd::flash_attn_bwd_set_knob(which, value);
-  });
+  // A/B knobs of the backward: 0 = ablation flags, 1 = chunk override (0 = auto)
+  m.def("flash_attn_set_knob", [](int which, int value) { nxd::flash_attn_bwd_set_knob(which, value); });
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("rope_inplace", &rope_inplace);

@@ -24,7 +24,9 @@
 //   * dQ: dS^T crosses LDS once; each wave computes one 32-wide d block of dS . K over the
 //     block's 256 keys (D=128; D=64 splits keys in halves and sums the halves in LDS) and adds
 //     it with f32 atomics into an fp32 dQ accumulator.  At 256 keys per block the atomic volume
-//     is one byte per 640 FLOPs (half of a 128-key design) — the kernel's floor.
+//     is one byte per 640 FLOPs (half of a 128-key design).  Not a floor: with the atomics,
+//     tile loads and barriers all ablated the body still runs only 839-930 TF/s
+//     (profiles/r2_fab_ablate_after.jsonl).
 #include "common.h"
 
 #include <algorithm>

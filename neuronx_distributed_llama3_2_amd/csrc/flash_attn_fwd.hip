@@ -45,8 +45,6 @@ struct FwdParams {
   float scale_log2;  // softmax_scale * log2(e)
   int causal;
   int causal_offset;  // query i attends keys <= i + causal_offset (Sk - Sq for bottom-right alignment)
-  int prio_hi;        // static s_setprio 1 for the second half of an 8-wave workgroup (MI355X_MICROARCH item 4)
-  int xcd_map;        // block -> (head, q block) map: 0 contiguous per XCD, 1 balanced kv-head-per-XCD, 2 interleaved
 };
 
 // 16-byte chunk swizzle of a [rows][D] bf16 LDS image (D/8 chunks per row).
@@ -83,69 +81,37 @@ __device__ __forceinline__ void tr_wait(short4_t (&v)[8]) {
                : "n"(N));
 }
 
-// lane l <-> l ^ 32 combine.  PIPE: v_permlane32_swap (VALU; the ds_bpermute of __shfl_xor would
-// make the compiler wait lgkmcnt(0) on the V reads already in flight) -> max (is_max) or sum of
-// the pair; otherwise the partner's value (__shfl_xor).
-template <bool PIPE>
+// lane l <-> l ^ 32 combine by v_permlane32_swap (VALU; the ds_bpermute of __shfl_xor would make
+// the compiler wait lgkmcnt(0) on the V reads already in flight) -> max (is_max) or sum of the pair.
 __device__ __forceinline__ float xor32(float x, bool is_max) {
-  if constexpr (PIPE) {
-    const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    const float a = __uint_as_float(pr[0]), b = __uint_as_float(pr[1]);
-    return is_max ? fmaxf(a, b) : a + b;
-  } else {
-    return __shfl_xor(x, 32, 64);
-  }
+  const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  const float a = __uint_as_float(pr[0]), b = __uint_as_float(pr[1]);
+  return is_max ? fmaxf(a, b) : a + b;
 }
 
-// NS = LDS ring stages (2, or 3 for the 8-wave variant: one workgroup per CU owns 96 KiB): tile
-// t + NS - 1 is DMA'd while tile t is computed; the loop-closing barrier waits (counted vmcnt) only
-// for tile t + 1.
-// KT = keys per LDS tile (64, or 128: two 64-key compute steps per barrier).
-template <int D, int W, bool PRIO, bool PIPE, int NS = 2, int KT = 64>
+// Double-buffered LDS ring of 64-key tiles: tile t + 1 is DMA'd while tile t is computed.
+template <int D, int W>
 __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
   constexpr int kWaves = W;
   constexpr int kBlockM = W * 32;                 // q rows per workgroup
   constexpr int CH = D / 8;                       // 16-B chunks per row
   constexpr int KS = D / 16;                      // k-steps of the QK^T product
   constexpr int NDB = D / 32;                     // 32-wide d blocks of O
-  constexpr int TILE_BYTES = KT * D * 2;          // one K (or V) LDS tile
+  constexpr int TILE_BYTES = kBlockN * D * 2;     // one K (or V) LDS tile
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // layout: [buf0: K | V][buf1: K | V]
 
+  // block -> (batch, q head, q block), interleaved over the XCDs: the dispatch order IS the
+  // heavy-first causal order and consecutive blocks land on different XCDs, so every XCD gets the
+  // same mix of block sizes (profiles/r2_fa_xcd_map_ab.jsonl: faster than contiguous ranges per XCD
+  // or kv-head-per-XCD maps at the TP=1 and TP=8 shapes)
   const int nblk_m = (p.Sq + kBlockM - 1) / kBlockM;
-  const int nwg = gridDim.x;
-  int b, hq, hkv, mblk;
-  if (p.xcd_map == 1) {
-    // Balanced XCD map (workgroup id x lands on XCD x % 8, in dispatch order x / 8): XCD x owns the
-    // kv heads {x, x + 8, ...} of every batch -- each XCD gets the SAME mix of causal block sizes
-    // (equal work per XCD) and every q head of a GQA group next to its K/V in one L2 -- walked
-    // heavy blocks first.  Needs B * Hkv % 8 == 0 (host-checked).
-    const int G = p.Hq / p.Hkv;
-    const int xcd = blockIdx.x & 7, i = blockIdx.x >> 3;
-    const int per_m = (p.B * p.Hkv / 8) * G;
-    mblk = nblk_m - 1 - i / per_m;
-    const int j = i % per_m;
-    const int bkv = (j / G) * 8 + xcd;
-    b = bkv / p.Hkv;
-    hkv = bkv % p.Hkv;
-    hq = hkv * G + j % G;
-  } else if (p.xcd_map == 2) {
-    // interleaved: dispatch order IS the heavy-first order, consecutive items on different XCDs
-    const int bh = blockIdx.x % (p.B * p.Hq);
-    mblk = nblk_m - 1 - blockIdx.x / (p.B * p.Hq);
-    b = bh / p.Hq;
-    hq = bh % p.Hq;
-    hkv = hq / (p.Hq / p.Hkv);
-  } else {
-    // contiguous ranges per XCD (round 1): XCD 0 receives the heaviest causal rows
-    const int L = xcd_remap(blockIdx.x, nwg);
-    const int bh = L % (p.B * p.Hq);
-    mblk = nblk_m - 1 - L / (p.B * p.Hq);  // heavy (late) causal blocks first
-    b = bh / p.Hq;
-    hq = bh % p.Hq;
-    hkv = hq / (p.Hq / p.Hkv);
-  }
+  const int bh = blockIdx.x % (p.B * p.Hq);
+  const int mblk = nblk_m - 1 - blockIdx.x / (p.B * p.Hq);
+  const int b = bh / p.Hq;
+  const int hq = bh % p.Hq;
+  const int hkv = hq / (p.Hq / p.Hkv);
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -172,7 +138,7 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
   // ---- key range
   int kend = p.Sk;
   if (p.causal) kend = min(p.Sk, qb0 + kBlockM + p.causal_offset);
-  const int ntiles = kend > 0 ? (kend + KT - 1) / KT : 0;
+  const int ntiles = kend > 0 ? (kend + kBlockN - 1) / kBlockN : 0;
   const int wave_qmax = q0 + 31 + p.causal_offset;  // last key any row of this wave may see
   const int wave_qmin = q0 + p.causal_offset;
 
@@ -196,7 +162,7 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
       const int piece = w * PIECES_PER_WAVE + i;
       const int row = piece * ROWS_PER_PIECE + lane / CH;
       const int ch = swz<D>(row, lane % CH);
-      const int key = min(t * KT + row, p.Sk - 1);
+      const int key = min(t * kBlockN + row, p.Sk - 1);
       const uint16_t* ks = kbase + (int64_t)key * p.k_ss + ch * 8;
       const uint16_t* vs = vbase + (int64_t)key * p.v_ss + ch * 8;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ks,
@@ -207,11 +173,9 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
   };
 
   if (ntiles > 0) issue_tile(0, 0);
-  if constexpr (NS > 2) {
-    for (int i = 1; i < NS - 1; ++i)
-      if (i < ntiles) issue_tile(i, i);
-  }
-  if (p.prio_hi && w >= kWaves / 2) __builtin_amdgcn_s_setprio(1);
+  // static priority for the younger half of an 8-wave workgroup (MI355X_MICROARCH "Two waves per
+  // SIMD" item 4); the condition is wave-uniform through readfirstlane (T5 static form)
+  if (kWaves == 8 && __builtin_amdgcn_readfirstlane(w) >= kWaves / 2) __builtin_amdgcn_s_setprio(1);
   __syncthreads();  // drains the LDS-DMA (vmcnt(0)) before any wave reads buffer 0
 
   // per-lane constant parts of the V transposed-read address (T10):
@@ -220,25 +184,23 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
   const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
   const int g = lane >> 4;
 
-  constexpr int LOADS_PER_TILE = 2 * PIECES_PER_WAVE;   // LDS-DMA instructions per thread per tile
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = NS == 2 ? (t & 1) : t % NS;
+    const int buf = t & 1;
     // buffer buf^1 was last read in iteration t-1, which every wave finished before the
     // barrier that closed it: safe to refill now, overlapped with this tile's MFMAs.
-    const bool issued = t + NS - 1 < ntiles;
-    if (issued) issue_tile(t + NS - 1, NS == 2 ? (buf ^ 1) : (t + NS - 1) % NS);
+    if (t + 1 < ntiles) issue_tile(t + 1, buf ^ 1);
 
-    for (int hf = 0; hf < KT / kBlockN; ++hf) {
-      const int kt0 = t * KT + hf * kBlockN;
+    {
+      const int kt0 = t * kBlockN;
       const bool wave_active = kt0 <= wave_qmax || !p.causal;
       if (wave_active) {
-        const char* kl = smem + buf * 2 * TILE_BYTES + hf * kBlockN * D * 2;
+        const char* kl = smem + buf * 2 * TILE_BYTES;
         const char* vl = kl + TILE_BYTES;
         // ---- S^T for the two 32-key subtiles
         f32x16_t sacc[2];
         sacc[0] = f32x16_t{0};
         sacc[1] = f32x16_t{0};
-        if constexpr (PIPE) {
+        {
           // K fragments one k-step ahead, both subtiles interleaved (two independent MFMA chains)
           u32x4_t kf[2][2];
           kf[0][0] = *reinterpret_cast<const u32x4_t*>(kl + lds_off<D>(r, hh));
@@ -252,22 +214,10 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
             sacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, kf[s & 1][0]), qf[s], sacc[0], 0, 0, 0);
             sacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, kf[s & 1][1]), qf[s], sacc[1], 0, 0, 0);
           }
-        } else {
-  #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int row = 32 * j + r;
-            if (PRIO && j == 0) __builtin_amdgcn_s_setprio(1);
-  #pragma unroll
-            for (int s = 0; s < KS; ++s) {
-              const u32x4_t kv = *reinterpret_cast<const u32x4_t*>(kl + lds_off<D>(row, 2 * s + hh));
-              sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, kv), qf[s], sacc[j], 0, 0, 0);
-            }
-          }
-          if (PRIO) __builtin_amdgcn_s_setprio(0);
         }
         // V reads of the first two P.V groups go out now, hidden behind the softmax VALU work
-        [[maybe_unused]] short4_t va[8], vb2[8];
-        [[maybe_unused]] const uint32_t vb = lds_addr(vl);
+        short4_t va[8], vb2[8];
+        const uint32_t vb = lds_addr(vl);
           // 4 groups (j, s2) of 8 transposed V reads (4 d-blocks x lo/hi); group g+1 is issued
           // before group g's MFMAs, a counted wait covers exactly group g
           auto issue = [&](int grp, short4_t (&v)[8]) {
@@ -281,16 +231,14 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
               v[2 * db + 1] = tr_read(vb + lds_off<D>(R0 + 8 + tq, ch) + sub);
             }
           };
-        if constexpr (PIPE) {
-          static_assert(NDB <= 4, "group size is 8 reads");
-          issue(0, va);
-          issue(1, vb2);
-        }
+        static_assert(NDB <= 4, "group size is 8 reads");
+        issue(0, va);
+        issue(1, vb2);
         // ---- mask + tile max on the RAW scores (scale > 0 commutes with max); the scale is folded
         // into one FMA per score below: p = exp2(s * c - m*c)
         const bool need_mask = (kt0 + kBlockN > p.Sk) || (p.causal && kt0 + kBlockN - 1 > wave_qmin);
         float tmax = -INFINITY;
-        if constexpr (PIPE) {
+        {
           // branch-free select against one per-lane limit: key offset c inside the tile is masked
           // iff c > lim (one compare + select per score, only on tiles that need a mask)
           if (need_mask) {
@@ -307,23 +255,8 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
           for (int j = 0; j < 2; ++j)
   #pragma unroll
             for (int e = 0; e < 16; ++e) tmax = fmaxf(tmax, sacc[j][e]);
-        } else {
-  #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-  #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-              float x = sacc[j][e];
-              if (need_mask) {
-                const int key = kt0 + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * hh;
-                const bool bad = key >= p.Sk || (p.causal && key > my_q + p.causal_offset);
-                x = bad ? -INFINITY : x;
-                sacc[j][e] = x;
-              }
-              tmax = fmaxf(tmax, x);
-            }
-          }
         }
-        tmax = fmaxf(tmax, xor32<PIPE>(tmax, true)) * p.scale_log2;
+        tmax = fmaxf(tmax, xor32(tmax, true)) * p.scale_log2;
         // deferred rescale (T13): keep the running max stale while the tile max exceeds it by less
         // than kRescaleThreshold (log2 units); p then stays below 2^threshold, fine in fp32 / bf16,
         // and the 4*NDB*16 accumulator multiplies are skipped on most tiles.
@@ -351,11 +284,11 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
             }
           }
         }
-        rsum = PIPE ? xor32<PIPE>(rsum, false) : rsum + __shfl_xor(rsum, 32, 64);
+        rsum = xor32(rsum, false);
         l_i += rsum;
 
         // ---- O^T += V^T P
-        if constexpr (PIPE) {
+        {
           auto mma = [&](int grp, short4_t (&v)[8]) {
             const int j = grp >> 1, s2 = grp & 1;
   #pragma unroll
@@ -375,42 +308,10 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
           mma(2, va);
           tr_wait<0>(vb2);
           mma(3, vb2);
-        } else {
-          if (PRIO) __builtin_amdgcn_s_setprio(1);
-  #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-  #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-              const int R0 = 32 * j + 16 * s2 + 4 * hh;  // this lane-half's first key of the k-step
-  #pragma unroll
-              for (int db = 0; db < NDB; ++db) {
-                const int col = 32 * db + 16 * (g & 1) + 4 * tp;
-                const int ch = col >> 3, sub = (col & 7) * 2;
-                const int ra = R0 + tq, rb = R0 + 8 + tq;
-                typedef __attribute__((address_space(3))) short4_t* lds_s4;
-                const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (lds_s4)(vl + lds_off<D>(ra, ch) + sub));
-                const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (lds_s4)(vl + lds_off<D>(rb, ch) + sub));
-                const short __attribute__((ext_vector_type(8))) a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                acc_o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a8), pf[j][s2], acc_o[db], 0, 0, 0);
-              }
-            }
-          }
-          if (PRIO) __builtin_amdgcn_s_setprio(0);
         }
       }
     }
-    if constexpr (NS == 2) {
-      __syncthreads();  // vmcnt(0) + barrier: tile t+1 has landed for every wave
-    } else {
-      // tile t+1 landed (this thread's share; the barrier makes it every thread's); the later
-      // tiles stay in flight.  "memory" keeps the compiler's LDS accesses on their side.
-      if (issued)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NS - 2) * LOADS_PER_TILE) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    }
+    __syncthreads();  // vmcnt(0) + barrier: tile t+1 has landed for every wave
   }
 
   // ---- epilogue: O[q][d] = acc / l ; lse
@@ -437,17 +338,6 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
 
 }  // namespace fa
 
-// NXD_FA_FWD_VARIANT resolved once at load; flash_attn_set_knob(2, v) switches it for A/B runs
-static int g_fwd_variant = -1;
-static int fwd_variant() {
-  if (g_fwd_variant < 0) {
-    const char* e = getenv("NXD_FA_FWD_VARIANT");
-    g_fwd_variant = e ? atoi(e) : 141;   // 13 | 128: interleaved block->XCD map (profiles/r2_fa_xcd_map_ab.jsonl)
-  }
-  return g_fwd_variant;
-}
-void flash_attn_fwd_set_variant(int v) { g_fwd_variant = v; }
-
 int flash_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse,
                           const int64_t* qs, const int64_t* ks, const int64_t* vs, const int64_t* os,
                           int B, int Sq, int Sk, int Hq, int Hkv, int D, float softmax_scale,
@@ -469,62 +359,22 @@ int flash_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, 
   p.causal_offset = causal_offset;
   if (Hkv <= 0 || Hq % Hkv != 0) return -1;
   if (D != 128 && D != 64) return -2;
-  // NXD_FA_FWD_VARIANT (A/B, re-read per launch; default 13).  Bits: 1 = 8-wave workgroups (only
-  // when the 256-row grid still fills the chip), 2 = s_setprio around the MFMA clusters, 4 =
-  // pipelined body (K reads one k-step ahead with two interleaved MFMA chains, branch-free mask,
-  // V transposed reads as asm issued before the softmax, permlane32 row reductions), 8 = static
-  // priority for waves 4-7, 16 = 3-stage LDS ring, 32 = 128-key LDS tiles.  Measured at S=8192
-  // D=128 causal, 32 / 4 heads (profiles/r1_fa_fwd_variants.jsonl): 0: 501 / 301 TF, 1: 531 / 298,
-  // 5: 578 / 411, 13: 574-587 / 406-417; 2, 16, 32 measured neutral or slower (kept selectable).
-  const int var = fwd_variant();
-  const bool prio = var & 2;
-  const bool pipe = var & 4;
-  const bool ring3 = (var & 16) && pipe;
-  const bool kt128 = (var & 32) && pipe;
-  p.prio_hi = (var & 8) ? 1 : 0;
-  // causal block-to-XCD map (variant bits 64/128): 64 = balanced kv-head-per-XCD when B * Hkv % 8 == 0
-  // (else interleaved), 128 = always interleaved, neither = contiguous ranges per XCD (round 1)
-  p.xcd_map = (var & 128) ? 2 : ((var & 64) ? (((B * Hkv) % 8 == 0) ? 1 : 2) : 0);
-  bool w8 = var & 1;
-  if (w8 && ((Sq + 255) / 256) * B * Hq < 512) w8 = false;
+  // 8-wave workgroups (256 query rows: half the K/V tile traffic and barriers per row) while the
+  // 256-row grid still fills the chip, else 4 waves.  Measured at S=8192 D=128 causal, 32 / 4 heads
+  // (profiles/r1_fa_fwd_variants.jsonl, profiles/r2_fa_xcd_map_ab.jsonl): this pipelined body
+  // 574-587 / 406-417 TF/s before the XCD map, 955-966 TF/s with it; the non-pipelined body, per-
+  // cluster s_setprio, a 3-stage LDS ring and 128-key tiles measured neutral or slower (removed).
+  const bool w8 = ((Sq + 255) / 256) * B * Hq >= 512;
   const int rows = w8 ? 256 : 128;
   const int grid = ((Sq + rows - 1) / rows) * B * Hq;
   if (grid == 0) return 0;
-  size_t lds = 2 * 2 * kBlockN * D * 2;
-#define NXD_FA_LAUNCH(DD, WW, PP, PI) \
-  hipLaunchKernelGGL((fwd_kernel<DD, WW, PP, PI>), dim3(grid), dim3(WW * 64), lds, stream, p)
-#define NXD_FA_LAUNCH_D(DD)                                                              \
-  if (pipe && w8 && kt128) {                                                             \
-    lds = 2 * 2 * 128 * DD * 2;                                                          \
-    static bool attr128_set_##DD = false;                                                \
-    if (!attr128_set_##DD) {                                                             \
-      attr128_set_##DD = true;                                                           \
-      (void)hipFuncSetAttribute((const void*)fwd_kernel<DD, 8, false, true, 2, 128>,     \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);   \
-    }                                                                                    \
-    hipLaunchKernelGGL((fwd_kernel<DD, 8, false, true, 2, 128>), dim3(grid), dim3(512), lds, stream, p); \
-  } else if (pipe && w8 && ring3) {                                                             \
-    lds = 3 * 2 * kBlockN * DD * 2;                                                      \
-    static bool attr_set_##DD = false;                                                   \
-    if (!attr_set_##DD) {                                                                \
-      attr_set_##DD = true;                                                              \
-      (void)hipFuncSetAttribute((const void*)fwd_kernel<DD, 8, false, true, 3>,          \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);   \
-    }                                                                                    \
-    hipLaunchKernelGGL((fwd_kernel<DD, 8, false, true, 3>), dim3(grid), dim3(512), lds, stream, p); \
-  } else if (pipe) {                                                                     \
-    if (w8) NXD_FA_LAUNCH(DD, 8, false, true); else NXD_FA_LAUNCH(DD, 4, false, true);   \
-  } else if (w8) {                                                                       \
-    if (prio) NXD_FA_LAUNCH(DD, 8, true, false); else NXD_FA_LAUNCH(DD, 8, false, false); \
-  } else {                                                                               \
-    if (prio) NXD_FA_LAUNCH(DD, 4, true, false); else NXD_FA_LAUNCH(DD, 4, false, false); \
-  }
+  const size_t lds = 2 * 2 * kBlockN * D * 2;
+#define NXD_FA_LAUNCH(DD, WW) hipLaunchKernelGGL((fwd_kernel<DD, WW>), dim3(grid), dim3(WW * 64), lds, stream, p)
   if (D == 128) {
-    NXD_FA_LAUNCH_D(128)
+    if (w8) NXD_FA_LAUNCH(128, 8); else NXD_FA_LAUNCH(128, 4);
   } else {
-    NXD_FA_LAUNCH_D(64)
+    if (w8) NXD_FA_LAUNCH(64, 8); else NXD_FA_LAUNCH(64, 4);
   }
-#undef NXD_FA_LAUNCH_D
 #undef NXD_FA_LAUNCH
   return (int)hipGetLastError();
 }

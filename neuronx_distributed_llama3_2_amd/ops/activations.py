@@ -40,7 +40,7 @@ class SwiGLUFunc(torch.autograd.Function):
             # next linear instead of h itself, see parallel_layers/layers.py)
             h_t = torch.empty((I, rows), dtype=gu.dtype, device=gu.device)
             ext().swiglu_fwd_dual(gu, h, h_t)
-            h._nxd_t = h_t
+            h._nxd_t, h._nxd_t_ver = h_t, h._version
         else:
             ext().swiglu_fwd(gu, h)
         ctx.save_for_backward(gu)
@@ -55,10 +55,20 @@ class SwiGLUFunc(torch.autograd.Function):
         if ctx.want_grad_t and _DUAL and rows and rows % 64 == 0 and (I2 // 2) % 64 == 0:
             dgu_t = torch.empty((I2, rows), dtype=gu.dtype, device=gu.device)
             ext().swiglu_bwd_dual(gu, dh.contiguous(), dgu, dgu_t)
-            dgu._nxd_t = dgu_t
+            dgu._nxd_t, dgu._nxd_t_ver = dgu_t, dgu._version
             return dgu, None, None
         ext().swiglu_bwd(gu, dh.contiguous(), dgu)
         return dgu, None, None
+
+
+def attached_token_major(x: torch.Tensor):
+    """The producer-written transposed copy attached to `x` (`x._nxd_t`), or None when there is
+    none or `x` was modified in place since it was written (in-place dropout, hooks, autograd
+    accumulation): the copy is then stale and the consumer must transpose `x` itself."""
+    t = getattr(x, "_nxd_t", None)
+    if t is None or getattr(x, "_nxd_t_ver", None) != x._version:
+        return None
+    return t
 
 
 def swiglu(gu: torch.Tensor, token_major: bool = False) -> torch.Tensor:

@@ -90,6 +90,7 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
                 buf = FlatBuffer(plist, dp_group=group, zero1=zero1, shared_ids=shared, name=f"g{gi}:{kind}" + (":ep" if is_ep else ""),
                                  avg_world=avg)
                 buf.kind = kind
+                buf.is_expert = is_ep
                 st = _BufferState(buf, g)
                 st.group_index = gi
                 st.param_index = [index_of[id(p)] for p in plist]   # registration order
@@ -158,11 +159,22 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
         tp_group, tp_rank = self._tp()
         dev = self.buffers[0].master.device
         total = torch.zeros(1, dtype=torch.float32, device=dev)
+        # without ZeRO-1 every DP rank holds whole buffers: dense ones are replicated over DP, but
+        # expert buffers hold only this EP rank's experts, so their part is summed over EP first
+        # (otherwise each EP rank clips with its own norm and the replicated dense params drift)
+        ep_group = None
+        if not self.zero1 and ps.model_parallel_is_initialized() and ps.get_expert_model_parallel_size() > 1:
+            ep_group = ps.get_expert_model_parallel_group()
+        ep_total = torch.zeros(1, dtype=torch.float32, device=dev) if ep_group is not None else total
         for b in self.buffers:
             if b.buf.kind != KIND_SHARDED and tp_rank != 0:
                 continue
+            acc = ep_total if getattr(b.buf, "is_expert", False) else total
             for s, e in b.ranges:
-                ops.flat_sumsq(b.buf.grad_data[s:e], out=total, accumulate=True)
+                ops.flat_sumsq(b.buf.grad_data[s:e], out=acc, accumulate=True)
+        if ep_group is not None:
+            dist.all_reduce(ep_total, group=ep_group)
+            total.add_(ep_total)
         if tp_group is not None:
             dist.all_reduce(total, group=tp_group)
         if self.zero1 and self.dp_group is not None and dist.get_world_size(group=self.dp_group) > 1:

@@ -204,12 +204,17 @@ class FlatBuffer:
         return out
 
     def gather_params(self) -> None:
-        """ZeRO-1: all-gather every bucket's updated bf16 slices (in place)."""
-        if not self.zero1:
-            return
+        """ZeRO-1: all-gather every bucket's updated bf16 slices (in place).
+
+        Every writer of `param_data` (optimizer steps, state-dict loads, DCP loads) calls this
+        afterwards, so this is where the GEMM layer's K-major weight copies are invalidated -- also
+        without ZeRO-1: writes through `param_data[s:e]` do not bump the params' own version
+        counters (they are views of the flat buffer), so nothing else would notice."""
         from ..ops.gemm import weights_updated
 
         weights_updated()
+        if not self.zero1:
+            return
         handles = []
         for b in self.buckets:
             n = (b.end - b.start) // self.dp

@@ -33,6 +33,7 @@ from torch.nn.parameter import Parameter
 
 from .. import ops
 from ..ops import gemm as _gemm
+from ..ops.activations import attached_token_major
 from . import sp
 from .mappings import (
     _gather_along_first_dim,
@@ -100,7 +101,7 @@ def _accumulate_wgrad(weight: torch.Tensor, go2: torch.Tensor, x2, go_t: torch.T
 
 def _token_major_copy(x: torch.Tensor):
     """The producer-written [K, tokens] copy of activation x ([..., K]) if one is attached."""
-    t = getattr(x, "_nxd_t", None)
+    t = attached_token_major(x)
     if t is None or t.dim() != 2 or not t.is_contiguous() or x.dim() < 1:
         return None
     K = x.shape[-1]
@@ -163,7 +164,7 @@ class LinearWithAsyncCommunication(torch.autograd.Function):
             total_input = sp.sp_gather(inp, ctx.process_group)
         else:
             total_input = inp
-        go_t = getattr(grad_output, "_nxd_t", None)   # token-contiguous copy from the SwiGLU backward
+        go_t = attached_token_major(grad_output)   # token-contiguous copy from the SwiGLU backward
         grad_output = grad_output.contiguous()
         group = ctx.process_group if ctx.process_group is not None else get_tensor_model_parallel_group()
         handles = []

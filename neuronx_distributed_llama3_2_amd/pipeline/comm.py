@@ -83,8 +83,8 @@ class P2PGroup:
         copy_in.clear()
         for t in tensors:
             self._exchange_of.pop(id(t), None)
-        if ex in self._inflight:
-            self._inflight.remove(ex)
+        # by identity: tuple == would compare the (possibly emptied) lists element-wise, i.e. tensors
+        self._inflight = [e for e in self._inflight if e is not ex]
 
     def wait_for(self, tensors) -> None:
         """Make the receive buffers in `tensors` safe to read (issues pending ops first)."""

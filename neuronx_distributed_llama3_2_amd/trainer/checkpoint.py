@@ -269,9 +269,11 @@ def save_checkpoint(checkpoint_dir_str: str, tag: str, model=None, optimizer=Non
         # reference trainer/checkpoint.py:496)
         group, gsize, grank = _model_replica_group()
         fn = os.path.join(str(tag), _get_path("model", ep=ep))
-        if use_xser and gsize > 1:
+        if use_xser and gsize > 1 and isinstance(storage, FilesysCheckpointStorage):
             # DP-deduplicated xser save (reference trainer/checkpoint.py:430-470): the replicas split
-            # the shard's tensor files by size; replica 0 also writes the structure and .info.pt
+            # the shard's tensor files by size; replica 0 also writes the structure and .info.pt.
+            # Filesystem only: object stores get one complete object from the single writer below
+            # (replicas writing partial objects to one key would overwrite each other).
             sd = _model_state(model)
             _tag_expert_tensors(model, sd)
             bins = assign_tensors_to_bins(xser_tensors(sd), gsize)
