@@ -57,6 +57,9 @@ int dgemv_launch(int, const void*, int64_t, const void*, float, const void*, int
                  int, int, const float*, const float*, const int64_t*, int, void*, void*, int64_t, int64_t, int64_t,
                  const int*, int, int, hipStream_t);
 int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, int, hipStream_t);
+int wgrad_gemm_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int, int, int, int, hipStream_t);
+int wgrad_gemm_choose_splits(int, int, int);
+void wgrad_gemm_set_ablate(int);
 int moe_combine_fwd_launch(const void*, const int64_t*, const float*, void*, int64_t, int, int, hipStream_t);
 int moe_combine_bwd_launch(const void*, const void*, const int64_t*, const float*, void*, float*, int64_t, int, int,
                            hipStream_t);
@@ -648,6 +651,27 @@ void dequant_int8(at::Tensor w, c10::optional<at::Tensor> scale, double tscale, 
            "dequant_int8");
 }
 
+// main_grad [M, N] fp32 += dy [T, M]^T x [T, N] (csrc/wgrad_gemm.hip): token-major bf16 operands with
+// unit inner strides, row strides multiples of 8 elements, T % 32 == 0; splits <= 0 -> auto.
+void wgrad_gemm(at::Tensor mg, at::Tensor dy, at::Tensor x, int64_t splits) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  check_cuda(mg, "main_grad");
+  TORCH_CHECK(mg.scalar_type() == at::kFloat, "wgrad_gemm: main_grad must be fp32");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && mg.dim() == 2, "wgrad_gemm: 2-D operands");
+  const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1);
+  TORCH_CHECK(x.size(0) == T && mg.size(0) == M && mg.size(1) == N, "wgrad_gemm: shape mismatch");
+  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1 && mg.stride(1) == 1, "wgrad_gemm: unit inner strides");
+  TORCH_CHECK(dy.stride(0) % 8 == 0 && x.stride(0) % 8 == 0, "wgrad_gemm: row strides must be multiples of 8");
+  TORCH_CHECK(T % 32 == 0 && M % 8 == 0 && N % 8 == 0, "wgrad_gemm: T % 32, M % 8, N % 8 must be 0");
+  TORCH_CHECK(T <= INT32_MAX && M <= INT32_MAX && N <= INT32_MAX, "wgrad_gemm: dims too large");
+  check_aligned16(dy, "dy");
+  check_aligned16(x, "x");
+  check_rc(nxd::wgrad_gemm_launch(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), mg.data_ptr<float>(),
+                                  mg.stride(0), (int)T, (int)M, (int)N, (int)splits, cur_stream()),
+           "wgrad_gemm");
+}
+
 // MoE grouped GEMMs over expert-sorted rows (csrc/grouped_gemm.hip); offs int32 [E + 1] on device.
 //   mode 0: a = x [M, K], b = W [E, K, N], c = y [M, N] bf16
 //   mode 1: a = dy [M, N], b = W [E, K, N], c = dx [M, K] bf16
@@ -822,6 +846,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("dequant_int8", &dequant_int8);
   m.def("expert_gemv", &expert_gemv);
   m.def("grouped_gemm", &grouped_gemm);
+  m.def("wgrad_gemm", &wgrad_gemm);
+  m.def("wgrad_gemm_set_ablate", [](int64_t v) { nxd::wgrad_gemm_set_ablate((int)v); });
+  m.def("wgrad_gemm_splits", [](int64_t T, int64_t M, int64_t N) { return nxd::wgrad_gemm_choose_splits((int)T, (int)M, (int)N); });
   m.def("moe_combine_fwd", &moe_combine_fwd);
   m.def("moe_combine_bwd", &moe_combine_bwd);
   m.def("dgemv", &dgemv);

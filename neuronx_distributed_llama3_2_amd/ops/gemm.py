@@ -76,6 +76,28 @@ def _use_wgrad_t(go2: torch.Tensor, x2: torch.Tensor = None, K: int = None) -> b
     return _WGRAD_T == "2" or N * K / (N + K) > 1200
 
 
+# Hand-written weight-gradient kernel (csrc/wgrad_gemm.hip): reads both token-major operands with
+# the hardware transpose read and splits the token range over workgroups.  Measured against this
+# module's hipBLASLt path (profiles/r3_wgrad_kernel_vs_hipblaslt.jsonl): faster on the skinny
+# tensor-parallel shards -- TP=8 qkv 984 vs 743 TF/s, o 880 vs 717 (M*N/(M+N) < 1100) -- and
+# 5-13 % slower on the large TP=1 shapes, so `auto` takes it only below that ratio.
+# NXD_WGRAD_KERNEL = auto | 1 (whenever the shapes allow) | 0.
+_WG_KERNEL = os.environ.get("NXD_WGRAD_KERNEL", "auto")
+_WG_SKINNY = 1100.0
+
+
+def _use_wgrad_kernel(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor) -> bool:
+    if _WG_KERNEL == "0" or x2 is None or not _native(go2, x2) or mg.dtype != torch.float32:
+        return False
+    T, M = go2.shape
+    N = x2.shape[1]
+    if T % 32 or M % 8 or N % 8 or go2.stride(1) != 1 or x2.stride(1) != 1 or mg.stride(1) != 1:
+        return False
+    if go2.stride(0) % 8 or x2.stride(0) % 8 or go2.data_ptr() % 16 or x2.data_ptr() % 16:
+        return False
+    return _WG_KERNEL == "1" or M * N / (M + N) < _WG_SKINNY
+
+
 def _wgrad_scratch(n: int, dtype, device, tag: str = "") -> torch.Tensor:
     key = (dtype, str(device), tag)
     t = _scratch.get(key)
@@ -96,6 +118,9 @@ def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2, go_t: torch.Tenso
     into a reused scratch, then an fp32 add (the per-micro-batch weight gradient is rounded to
     bf16 before the fp32 accumulation — the precision of the reference's XLA matmul + fp32
     grad accumulation; hipBLASLt's bf16-output solutions run faster than its fp32-output ones)."""
+    if _use_wgrad_kernel(mg, go2, x2):
+        ext().wgrad_gemm(mg, go2, x2, 0)
+        return
     if x_t is not None and not (x_t.dim() == 2 and x_t.is_contiguous() and x_t.shape[1] == go2.shape[0]):
         x_t = None
     if x2 is None and not (x_t is not None and _native(go2, x_t) and mg.is_contiguous()
