@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--layers", type=int, default=None, help="override #layers (NOT the headline config)")
     ap.add_argument("--no-sp", action="store_true")
     ap.add_argument("--ckpt", default=None, help="activation checkpointing: None | full | selective")
+    ap.add_argument("--lr", type=float, default=1e-5, help="AdamW learning rate (tests raise it so the loss moves)")
     ap.add_argument("--cpu", action="store_true", help="force the CPU/gloo path (plumbing tests)")
     ap.add_argument("--gloo-gpu", action="store_true",
                     help="test mode: every rank on cuda:0 with gloo collectives on staged GPU tensors (multi-rank "
@@ -122,7 +123,7 @@ def _build_pipeline(a, cfg, tp, n_micro, dev, dtype):
                                 "use_master_weights_in_ckpt": False})
     model = nxd.initialize_parallel_model(nxd_config, LlamaForCausalLM, cfg, dtype=dtype, device=dev)
     groups = get_param_groups_by_weight_decay(model, 0.01)
-    opt = nxd.initialize_parallel_optimizer(nxd_config, torch.optim.AdamW, groups, lr=1e-5, betas=(0.9, 0.95), eps=1e-8)
+    opt = nxd.initialize_parallel_optimizer(nxd_config, torch.optim.AdamW, groups, lr=a.lr, betas=(0.9, 0.95), eps=1e-8)
     assert ps.get_pipeline_model_parallel_size() == a.pp
     return model, opt
 
@@ -206,15 +207,21 @@ def main(a):
         decay = [p for n, p in model.named_parameters() if p.dim() > 1]
         no_decay = [p for n, p in model.named_parameters() if p.dim() <= 1]
         opt = FlatMixedPrecisionAdamW([{"params": decay, "weight_decay": 0.01}, {"params": no_decay, "weight_decay": 0.0}],
-                                      lr=1e-5, betas=(0.9, 0.95), eps=1e-8, zero1=dp > 1, grad_clipping=True,
+                                      lr=a.lr, betas=(0.9, 0.95), eps=1e-8, zero1=dp > 1, grad_clipping=True,
                                       max_grad_norm=1.0, shared_param_ids=find_shared_params(model))
     nparams_local = sum(p.numel() for p in model.parameters())
     # a fresh batch for every micro-step of every step (warmup included), generated before the timed
-    # region; identical across the TP ranks of one DP rank, different across DP ranks.  Random tokens
-    # cannot be memorised, so the reported loss stays near ln(V) and flags numerics regressions.
-    g = torch.Generator(device="cpu").manual_seed(4321 + ps.get_data_parallel_rank())
-    n_micro = accum * (a.warmup + a.steps)
-    batches = torch.randint(0, cfg.vocab_size, (n_micro, a.mbs, a.seq), generator=g).to(dev)
+    # region; identical across the TP ranks of one DP rank.  Random tokens cannot be memorised, so
+    # at the default learning rate the reported loss stays near ln(V) and flags numerics regressions.
+    # One global token stream for every layout: step k's global batch is the same gbs sequences at
+    # any TP / PP / DP split (DP rank r takes its contiguous share), so runs are comparable.
+    g = torch.Generator(device="cpu").manual_seed(4321)
+    n_steps = a.warmup + a.steps
+    stream = torch.randint(0, cfg.vocab_size, (n_steps, a.gbs, a.seq), generator=g)
+    share = a.gbs // dp
+    r0 = ps.get_data_parallel_rank() * share
+    batches = stream[:, r0:r0 + share].reshape(n_steps * accum, a.mbs, a.seq).to(dev)
+    del stream
     cursor = [0]
 
     def train_step():
@@ -226,15 +233,17 @@ def main(a):
             opt.step()
             opt.zero_grad()
             return loss
+        tot = None
         for i in range(accum):
             opt.set_grad_sync(i == accum - 1)
             ids = batches[cursor[0]]
             cursor[0] += 1
             out = model(ids, labels=ids)
             (out.loss / accum).backward()
+            tot = out.loss.detach() if tot is None else tot + out.loss.detach()
         opt.step()
         opt.zero_grad()
-        return out.loss
+        return tot / accum   # mean over the step's micro-batches (= the pipeline path's loss)
 
     for _ in range(a.warmup):
         loss = train_step()

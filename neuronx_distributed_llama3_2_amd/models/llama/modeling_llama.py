@@ -102,7 +102,13 @@ class LlamaAttention(nn.Module):
             sequence_parallel_enabled=sp, kv_size_multiplier=kv_mult, fuse_qkv=True, dtype=dtype, device=device)
         self.o_proj = RowParallelLinear(self.num_heads * self.head_dim, self.hidden_size,
                                         bias=getattr(config, "attention_bias", False), input_is_parallel=True,
-                                        init_method=init, sequence_parallel_enabled=sp, dtype=dtype, device=device)
+                                        init_method=init, sequence_parallel_enabled=sp, dtype=dtype, device=device,
+                                        keep_master_weight=kv_mult > 1)
+        if kv_mult > 1:
+            # replicated kv heads: this rank's q heads are head group q_group_order[rank] (see
+            # qkv_proj), so its o_proj input columns are that group's (reference
+            # scripts/checkpoint_converter.py:463-481 reshuffles o_proj the same way)
+            _regroup_row_parallel(self.o_proj, tp, kv_mult)
         self.rope_cache = rope_cache
 
     def forward(self, x):
@@ -111,6 +117,19 @@ class LlamaAttention(nn.Module):
         o = ops.rope_attention(qkv, cos_t, sin_t, self.num_heads_local, self.num_kv_heads_local, self.head_dim,
                                causal=True)
         return self.o_proj(o)
+
+
+def _regroup_row_parallel(layer, tp: int, mult: int) -> None:
+    from ...parallel_layers.parallel_state import get_tensor_model_parallel_rank
+    from ...parallel_layers.sharding import q_group_order
+
+    layer.weight.qkv_qgroup_mult = mult
+    master = getattr(layer, "master_weight", None)
+    if master is not None and layer.weight.device.type != "meta":
+        g = q_group_order(tp, mult)[get_tensor_model_parallel_rank()]
+        with torch.no_grad():
+            layer.weight.copy_(torch.chunk(master, tp, dim=1)[g])
+    layer.master_weight = None
 
 
 class RopeCache:

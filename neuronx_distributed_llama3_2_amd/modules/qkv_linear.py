@@ -170,11 +170,16 @@ class GQAQKVColumnParallelLinear(BaseParallelLinear):
 
     # full weights are generated deterministically (same on every rank) then sharded
     def _shard_full(self, full: torch.Tensor, is_kv: bool) -> torch.Tensor:
+        """Same layout as parallel_layers.sharding.shard_tensor: replicated K/V, and with
+        replication each rank's Q head group is the one that attends to its kv head."""
+        from ..parallel_layers.sharding import q_group_order
+
         ws, rank = get_tensor_model_parallel_size(), get_tensor_model_parallel_rank()
         if is_kv and self.kv_size_multiplier > 1:
             full = torch.cat([full] * self.kv_size_multiplier, dim=0)
         per = full.shape[0] // ws
-        return full[rank * per:(rank + 1) * per]
+        g = q_group_order(ws, self.kv_size_multiplier)[rank] if not is_kv else rank
+        return full[g * per:(g + 1) * per]
 
     def _init_full(self, rows: int) -> torch.Tensor:
         w = torch.empty(rows, self.input_size, dtype=torch.float32, device=self.device if self.device.type != "meta" else "cpu")

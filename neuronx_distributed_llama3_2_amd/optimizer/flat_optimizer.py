@@ -47,6 +47,26 @@ class _BufferState:
         self.exp_avg_sq = torch.zeros_like(self.master)
 
 
+def replica_slices(buf, ranges):
+    """(start, end, weight) pieces of `ranges` (flat offsets of `buf`) that hold the K/V rows of a
+    GQA QKV projection whose kv heads are replicated on m TP ranks (weight 1/m, grads.py)."""
+    from ..parallel_layers.grads import kv_replica_slices
+
+    out = []
+    for p in buf.params:
+        kv = kv_replica_slices(p)
+        if kv is None:
+            continue
+        off, n = buf.offsets[id(p)]
+        cols = p.shape[1] if p.dim() > 1 else 1
+        ks, ke = off + kv[0] * cols, off + n
+        for s, e in ranges:
+            lo, hi = max(s, ks), min(e, ke)
+            if lo < hi:
+                out.append((lo, hi, kv[1]))
+    return out
+
+
 class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
     """AdamW (decoupled weight decay) with fp32 master weights over flat buffers; optional ZeRO-1.
 
@@ -172,6 +192,10 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
             acc = ep_total if getattr(b.buf, "is_expert", False) else total
             for s, e in b.ranges:
                 ops.flat_sumsq(b.buf.grad_data[s:e], out=acc, accumulate=True)
+            for lo, hi, w in self._replica_slices(b):   # replicated K/V rows count 1/m (grads.py)
+                tmp = torch.zeros(1, dtype=torch.float32, device=dev)
+                ops.flat_sumsq(b.buf.grad_data[lo:hi], out=tmp, accumulate=True)
+                acc.add_(tmp, alpha=w - 1.0)
         if ep_group is not None:
             dist.all_reduce(ep_total, group=ep_group)
             total.add_(ep_total)
@@ -182,6 +206,13 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
         if ps.model_parallel_is_initialized() and ps.get_pipeline_model_parallel_size() > 1:
             dist.all_reduce(total, group=ps.get_pipeline_model_parallel_group())
         return total
+
+    def _replica_slices(self, b):
+        """Flat (start, end, weight) pieces of this rank's shard that hold kv-replicated K/V rows."""
+        cached = getattr(b, "_replica_cache", None)
+        if cached is None:
+            cached = b._replica_cache = replica_slices(b.buf, b.ranges)
+        return cached
 
     @torch.no_grad()
     def step(self, closure=None):

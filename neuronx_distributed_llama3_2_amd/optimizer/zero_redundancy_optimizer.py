@@ -26,7 +26,7 @@ import torch.distributed as dist
 from .. import ops
 from ..parallel.grad_buffer import KIND_DUP_SP, KIND_SHARDED, FlatBuffer, param_kind
 from ..parallel_layers import parallel_state as ps
-from .flat_optimizer import FlatMixedPrecisionAdamW
+from .flat_optimizer import FlatMixedPrecisionAdamW, replica_slices
 
 _ADAM_NAMES = {"AdamW", "Adam", "AdamW_FP32OptimParams", "FusedAdam"}
 
@@ -98,6 +98,10 @@ class _GenericZero1(torch.optim.Optimizer):
                     continue
                 for m in masters:
                     ops.flat_sumsq(m.grad, out=sq, accumulate=True)
+                for lo, hi, w in replica_slices(b, [m._range for m in masters]):   # replicated K/V rows
+                    tmp = torch.zeros(1, dtype=torch.float32, device=dev)
+                    ops.flat_sumsq(b.grad_data[lo:hi], out=tmp, accumulate=True)
+                    sq.add_(tmp, alpha=w - 1.0)
             if tp > 1:
                 dist.all_reduce(sq, group=ps.get_tensor_model_parallel_group())
             if self.dp_group is not None and dist.get_world_size(group=self.dp_group) > 1:

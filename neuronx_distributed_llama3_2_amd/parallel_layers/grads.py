@@ -5,7 +5,10 @@
   HIP kernel when gradients live in one buffer) — not one `torch.norm` per tensor; the result stays
   on the device (no host sync) and clipping multiplies by a device-side coefficient.
 * TP-duplicated parameters (norm weights, row-parallel biases) are counted once (on TP rank 0),
-  TP-sharded ones on every rank, then the partial sums are all-reduced over TP and PP.
+  TP-sharded ones on every rank, then the partial sums are all-reduced over TP and PP.  K/V rows
+  of a GQA QKV projection whose kv heads are replicated on m ranks (`qkv_split[2] = m`) are the
+  same parameter m times: their squares count 1/m on each replica, so the norm (and clipping) is
+  the unsharded model's at every TP degree.  (The reference counts them m times.)
 * DP reduction coalesces gradients into per-dtype buckets (default 128 MiB:
   `ALLREDUCE_BUCKET_CAP_MB`) — sized so each RCCL ring chunk over the 7 xGMI links stays in the
   bandwidth regime — reduced in reverse registration order.
@@ -52,6 +55,16 @@ def _grad_of(p):
     return g if g is not None else p.grad
 
 
+def kv_replica_slices(p):
+    """(first row, weight) of the replicated K/V rows of a fused GQA QKV weight/bias `p`: rows from
+    `first row` on are kv heads held by `m` ranks each, weight 1/m.  None for other parameters."""
+    qs = getattr(p, "qkv_split", None)
+    if not qs or int(qs[2]) <= 1 or not model_parallel_is_initialized():
+        return None
+    q_rows, _, mult = qs
+    return q_rows // get_tensor_model_parallel_size(), 1.0 / float(mult)
+
+
 def get_grad_norm(parameters, norm_type: float = 2, zero1_optimizer: bool = False, zero1_optimizer_groups=None,
                   force_spmd: bool = True) -> torch.Tensor:
     """Global gradient norm (device tensor) over every model-parallel dimension."""
@@ -71,7 +84,13 @@ def get_grad_norm(parameters, norm_type: float = 2, zero1_optimizer: bool = Fals
         if norm_type == float("inf"):
             return torch.stack([g.detach().abs().max().float() for g in grads]).max().reshape(1)
         norms = torch._foreach_norm([g.detach() for g in grads], norm_type)
-        return torch.stack([n.float() for n in norms]).pow(norm_type).sum().reshape(1)
+        tot = torch.stack([n.float() for n in norms]).pow(norm_type).sum().reshape(1)
+        for p in ps:   # replicated K/V rows count 1/m per replica
+            kv = kv_replica_slices(p)
+            if kv is not None:
+                g = _grad_of(p).detach()[kv[0]:]
+                tot = tot - (1.0 - kv[1]) * g.float().norm(norm_type).pow(norm_type)
+        return tot
 
     op = dist.ReduceOp.MAX if norm_type == float("inf") else dist.ReduceOp.SUM
     total = local_stat(dense)

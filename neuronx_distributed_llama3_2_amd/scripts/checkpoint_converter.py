@@ -59,7 +59,9 @@ class CheckpointConverterBase:
                 return {"tp": True, "dim": 1, "stride": 1, "qkv": None, "ep": True}
         if "gate_up_proj.weight" in name:
             return {"tp": True, "dim": 0, "stride": 2, "qkv": None}
-        if name.endswith(("o_proj.weight", "down_proj.weight")):
+        if name.endswith("o_proj.weight"):   # head groups follow the Q reshuffle of replicated kv heads
+            return {"tp": True, "dim": 1, "stride": 1, "qkv": None, "qgroup_mult": kv_mult}
+        if name.endswith("down_proj.weight"):
             return {"tp": True, "dim": 1, "stride": 1, "qkv": None}
         return rep
 

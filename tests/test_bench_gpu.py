@@ -20,7 +20,10 @@ def _run(n, *extra, model="tiny"):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
-    args = ["--model", model, "--seq", "512", "--gbs", "8", "--steps", "2", "--warmup", "1", "--gloo-gpu", *extra]
+    # lr 3e-3: three AdamW steps move the loss away from ln V, so the final loss is a check of the
+    # sharded gradients (same token stream for every TP / PP layout of one DP rank)
+    args = ["--model", model, "--seq", "512", "--gbs", "8", "--steps", "2", "--warmup", "1", "--lr", "3e-3",
+            "--gloo-gpu", *extra]
     r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), *args], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -29,21 +32,35 @@ def _run(n, *extra, model="tiny"):
     return recs[0]
 
 
+_REF = {}
+
+
+def _tp1(model, *extra):
+    key = (model, extra)
+    if key not in _REF:
+        _REF[key] = _run(1, *extra, model=model)
+    return _REF[key]
+
+
 @pytest.mark.parametrize("n", [2, 4, 8])
 def test_bench_tp_sp_ranks_on_one_gpu(n):
     rec = _run(n, model="tiny8")     # 16 / 8 heads: one KV head per rank at TP = 8, as the headline
     assert rec["config"]["parallelism"] == f"tp{n}_sp" and rec["n_gpus"] == n and rec["comm_world_size"] == n
-    assert rec["value"] > 0 and abs(rec["loss"] - math.log(1024)) < 0.5, rec
+    ref = _tp1("tiny8")
+    assert rec["value"] > 0 and abs(rec["loss"] - math.log(1024)) > 0.02, rec   # the loss moved
+    assert abs(rec["loss"] - ref["loss"]) < 1e-2 * ref["loss"], (rec["loss"], ref["loss"])
 
 
 def test_bench_dp_zero1_ranks_on_one_gpu():
     rec = _run(2, "--parallelism", "dp")
     assert rec["config"]["parallelism"] == "tp1_dp2_zero1" and rec["value"] > 0
-    assert abs(rec["loss"] - math.log(1024)) < 0.5, rec
+    ref = _tp1("tiny")     # same global batches: DP rank r takes its share of one token stream
+    assert abs(rec["loss"] - ref["loss"]) < 1e-2 * ref["loss"], (rec["loss"], ref["loss"])
 
 
 def test_bench_pipeline_ranks_on_one_gpu():
     """TP=2 x PP=2 NxDPPModel 1F1B through bench.py --pp on the GPU kernels."""
     rec = _run(4, "--pp", "2")
     assert rec["config"]["parallelism"] == "tp2_sp_pp2_1f1b" and rec["value"] > 0
-    assert abs(rec["loss"] - math.log(1024)) < 0.5, rec
+    ref = _tp1("tiny")
+    assert abs(rec["loss"] - ref["loss"]) < 1e-2 * ref["loss"], (rec["loss"], ref["loss"])

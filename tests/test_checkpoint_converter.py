@@ -81,12 +81,14 @@ def test_sharded_checkpoint_loads_into_tp_model():
     with open(cfg_path, "w") as f:
         json.dump(cfg.to_dict(), f)
     torch.save(sd, os.path.join(d, "checkpoint.pt"))
-    for tp in (1, 2):
+    # TP=4 over 2 kv heads replicates each kv head on 2 ranks: the converter's Q-head reshuffle
+    # makes the replicated layout compute the unsharded model
+    for tp, mult in ((1, 1), (2, 1), (4, 2)):
         _run(["--input_dir", d, "--output_dir", os.path.join(d, f"tp{tp}"), "--config", cfg_path, "--tp_size", str(tp),
-              "--convert_from_full_state"])
+              "--kv_size_multiplier", str(mult), "--convert_from_full_state"])
         run_distributed(_w_load_shards, tp, os.path.join(d, f"tp{tp}"), cfg.to_dict(), os.path.join(d, f"l{tp}.pt"))
-    a, b = torch.load(os.path.join(d, "l1.pt")), torch.load(os.path.join(d, "l2.pt"))
-    assert abs(a - b) < 1e-4, (a, b)
+    a, b, c = (torch.load(os.path.join(d, f"l{t}.pt")) for t in (1, 2, 4))
+    assert abs(a - b) < 1e-4 and abs(a - c) < 1e-4, (a, b, c)
     # and the TP=1 framework model reproduces HF's loss on the same weights
     from transformers import LlamaForCausalLM as HF
 

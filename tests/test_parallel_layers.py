@@ -210,3 +210,41 @@ def test_tiny_llama_tp8_sp_matches_tp1():
     r8 = torch.load(f"/tmp/nxd_tiny_llama_8_True_0{_tag(over)}.pt")
     torch.testing.assert_close(r1["loss"], r8["loss"], atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(r1["gn"], r8["gn"], atol=1e-3, rtol=1e-3)
+
+
+def _w_kv_replicated_training(rank, world, out):
+    """TP > #kv heads: replicated kv heads (q head groups reshuffled as the reference converter does)
+    train exactly like the unsharded model, clip norm included (replicated K/V rows count once)."""
+    from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
+    from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW
+    from neuronx_distributed_llama3_2_amd.parallel.grad_buffer import find_shared_params
+
+    ps.initialize_model_parallel(world)
+    cfg = llama_config("tiny", sequence_parallel_enabled=world > 1, max_position_embeddings=512)
+    torch.manual_seed(0)
+    model = LlamaForCausalLM(cfg, dtype=torch.float32, device=torch.device("cpu"))
+    opt = FlatMixedPrecisionAdamW(model.parameters(), lr=2e-3, grad_clipping=True, max_grad_norm=1.0,
+                                  shared_param_ids=find_shared_params(model))
+    torch.manual_seed(5)
+    ids = torch.randint(0, cfg.vocab_size, (2, 64))
+    res = []
+    for _ in range(3):
+        loss = model(ids, labels=ids).loss
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        res.append((float(loss), float(opt.grad_norm)))
+    if rank == 0:
+        torch.save(res, out)
+
+
+def test_kv_replicated_tp4_trains_like_tp1():
+    import os
+    import tempfile
+
+    d = tempfile.mkdtemp()
+    run_distributed(_w_kv_replicated_training, 1, os.path.join(d, "a.pt"))
+    run_distributed(_w_kv_replicated_training, 4, os.path.join(d, "b.pt"))   # tiny: 2 kv heads, m = 2
+    a, b = torch.load(os.path.join(d, "a.pt")), torch.load(os.path.join(d, "b.pt"))
+    for (la, ga), (lb, gb) in zip(a, b):
+        assert abs(la - lb) < 1e-4 and abs(ga - gb) < 1e-4 * ga, (a, b)
