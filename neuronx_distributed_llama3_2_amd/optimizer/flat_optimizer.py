@@ -246,6 +246,15 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
 
     # ---------------------------------------------------------------- checkpointing
     def state_dict(self) -> Dict[str, Any]:
+        """The reference's layout (optimizer/zero_layout.py): torch_xla ZeRO-1 per-parameter dim-0
+        shards with `base_state` / `shape_info` / `sharded_master_weights` under ZeRO-1, the plain
+        torch layout (+ `master_weights`) without.  Collective over the DP group under ZeRO-1."""
+        from .zero_layout import reference_state_dict
+
+        return reference_state_dict(self)
+
+    def flat_state_dict(self) -> Dict[str, Any]:
+        """This rank's flat buffers as they are (no communication; the layout of round-2 files)."""
         groups = [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]
         bufs = []
         for b in self.buffers:
@@ -257,25 +266,35 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
         return {"flat_optimizer": True, "step": self.step_count, "param_groups": groups, "buffers": bufs,
                 "zero1": self.zero1}
 
-    def load_state_dict(self, sd: Dict[str, Any]) -> None:
-        if sd.get("flat_optimizer_full"):
-            return self._load_full_state_dict(sd)
-        assert sd.get("flat_optimizer"), "not a FlatMixedPrecisionAdamW state dict"
-        self.step_count = int(sd["step"])
+    def _after_load(self) -> None:
         if self.capturable:
             self._dev_step.fill_(float(self.step_count))
+        self.sync_lr()
+        for b in self.buffers:
+            for (s, e, lo) in b.local:
+                b.buf.param_data[s:e].copy_(b.master[lo:lo + e - s])
+            b.buf.gather_params()
+
+    def load_state_dict(self, sd: Dict[str, Any]) -> None:
+        from .zero_layout import is_reference_layout, load_reference_state_dict
+
+        if sd.get("flat_optimizer_full"):
+            return self._load_full_state_dict(sd)
+        if not sd.get("flat_optimizer") and is_reference_layout(sd):
+            self.step_count = load_reference_state_dict(self, sd)
+            self._after_load()
+            return
+        assert sd.get("flat_optimizer"), "not a FlatMixedPrecisionAdamW state dict"
+        self.step_count = int(sd["step"])
         for g, sg in zip(self.param_groups, sd["param_groups"]):
             for k, v in sg.items():
                 g[k] = v
-        self.sync_lr()
         for b, sb in zip(self.buffers, sd["buffers"]):
             assert b.buf.name == sb["name"] and b.master.numel() == sb["master"].numel(), "optimizer layout mismatch"
             b.master.copy_(sb["master"])
             b.exp_avg.copy_(sb["exp_avg"])
             b.exp_avg_sq.copy_(sb["exp_avg_sq"])
-            for (s, e, lo) in b.local:
-                b.buf.param_data[s:e].copy_(b.master[lo:lo + e - s])
-            b.buf.gather_params()
+        self._after_load()
 
     def _load_full_state_dict(self, sd: Dict[str, Any]) -> None:
         """DP-agnostic state (optimizer/convert_zero_checkpoints.py "full" format): per-parameter

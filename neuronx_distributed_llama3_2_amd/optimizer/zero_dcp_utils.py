@@ -1,14 +1,15 @@
 """ZeRO-1 optimizer state through torch.distributed.checkpoint (DCP)
 (reference: src/neuronx_distributed/optimizer/zero_dcp_utils.py:84-519).
 
-Every flat optimizer buffer (fp32 master / exp_avg / exp_avg_sq of one (param group, kind) on one
-(TP, PP) rank) is exposed to DCP as ONE global 1-D ShardedTensor whose local shards are exactly
-this DP rank's bucket slices — so `save_optim_state_dict` writes each byte once (no gather) and
-`load_optim_state_dict` reads whatever slices the CURRENT layout needs, i.e. loading with a
-different DP size re-shards on the fly as long as the bucket plan is identical (same DP-agnostic
-padding is not guaranteed across DP sizes: for DP changes use the DP-agnostic "full" format of
-optimizer/convert_zero_checkpoints.py; DCP covers same-layout save/load and partial reads).
-Keys carry the (TP, PP) coordinates so ranks of different model shards never collide.
+Like the reference (`_tensor_to_sharded_tensor`, :84-140), every parameter's fp32 master / exp_avg /
+exp_avg_sq is exposed to DCP as one ShardedTensor of the parameter's GLOBAL shape, row-sharded
+along dim 0 over the data-parallel group (DP rank r owns rows [r c, (r + 1) c), c = ceil(rows /
+DP): the torch_xla ZeRO shard without its padding).  Save writes each row once; load describes the
+rows the CURRENT DP layout needs, so a checkpoint saved at one DP size loads at any other (DCP
+re-slices), then the per-parameter rows are turned back into the flat ZeRO-1 buffer slices
+(optimizer/zero_layout.py, one all-gather per bucket).  Keys carry the (TP, PP) coordinates
+(`tpXX_ppXX.pN.field`, the reference's `|pp-XXXX|tp-XXXX` fqn suffix, :196-209) so ranks of
+different model shards never collide; the step and param-group hyper-parameters are plain entries.
 """
 
 from __future__ import annotations
@@ -32,33 +33,46 @@ def _coords() -> str:
     return "tp00_pp00"
 
 
-def _sharded(buf_state, field: str, group) -> Any:
-    t = getattr(buf_state, field)
-    rank = dist.get_rank()
+def _rows(d0: int, dp: int, r: int):
+    c = -(-d0 // dp)
+    return min(r * c, d0), min((r + 1) * c, d0)
+
+
+def _sharded_param(t: torch.Tensor, shape, dp: int, r: int, group) -> Any:
+    """ShardedTensor of global `shape` whose local shard is rows _rows(...) of `t` (full tensor)."""
+    lo, hi = _rows(shape[0], dp, r)
     shards = []
-    for (s, e, lo) in buf_state.local:
-        shards.append(Shard(tensor=t[lo:lo + e - s], metadata=ShardMetadata(shard_offsets=[s], shard_sizes=[e - s],
-                                                                          placement=f"rank:{rank}/{t.device}")))
-    return init_from_local_shards(shards, buf_state.buf.numel, process_group=group)
+    if hi > lo:
+        off = [lo] + [0] * (len(shape) - 1)
+        size = [hi - lo] + list(shape[1:])
+        shards.append(Shard(tensor=t[lo:hi].contiguous(),
+                            metadata=ShardMetadata(shard_offsets=off, shard_sizes=size,
+                                                   placement=f"rank:{dist.get_rank()}/{t.device}")))
+    return init_from_local_shards(shards, *shape, process_group=group)
 
 
-def _state(optimizer) -> Dict[str, Any]:
+def _group(b):
+    return b.buf.dp_group if b.buf.dp > 1 else None
+
+
+def _save_state(optimizer) -> Dict[str, Any]:
+    from .zero_layout import full_states, param_entries
+
     c = _coords()
     sd: Dict[str, Any] = {f"{c}.step": torch.tensor(float(optimizer.step_count))}
-    for i, b in enumerate(optimizer.buffers):
-        group = b.buf.dp_group if b.buf.dp > 1 else None
-        for f in _FIELDS:
-            if b.buf.zero1:
-                sd[f"{c}.buf{i}.{f}"] = _sharded(b, f, group)
-            else:
-                sd[f"{c}.buf{i}.{f}.r{dist.get_rank()}"] = getattr(b, f)
+    index = {id(p): i for (i, _, p, _) in param_entries(optimizer)}
+    for b in optimizer.buffers:
+        for p, full in full_states(b):
+            i = index[id(p)]
+            for f in _FIELDS:
+                sd[f"{c}.p{i}.{f}"] = _sharded_param(full[f], tuple(full[f].shape), b.buf.dp, b.buf.dp_rank, _group(b))
     return sd
 
 
 def save_optim_state_dict(path: str, optimizer, **kwargs) -> None:
-    """Collective: every rank writes its own slices under `path` (a directory)."""
+    """Collective: every rank writes its own parameter rows under `path` (a directory)."""
     os.makedirs(path, exist_ok=True)
-    dcp.save(_state(optimizer), checkpoint_id=path)
+    dcp.save(_save_state(optimizer), checkpoint_id=path)
     if dist.get_rank() == 0:
         groups = [{k: v for k, v in g.items() if k != "params"} for g in optimizer.param_groups]
         torch.save({"param_groups": groups}, os.path.join(path, "nxd_param_groups.pt"))
@@ -66,16 +80,35 @@ def save_optim_state_dict(path: str, optimizer, **kwargs) -> None:
 
 
 def load_optim_state_dict(path: str, optimizer, **kwargs) -> None:
-    """Collective: fills every rank's master / moment slices in place, then refreshes the bf16
-    parameters from the loaded master weights."""
-    sd = _state(optimizer)
-    dcp.load(sd, checkpoint_id=path)
+    """Collective: reads the rows this rank's CURRENT DP layout owns (any DP size at save time),
+    rebuilds the flat ZeRO-1 slices and refreshes the bf16 parameters from the loaded master."""
+    from .zero_layout import load_full_states, param_entries
+
     c = _coords()
+    entries = param_entries(optimizer)
+    sd: Dict[str, Any] = {f"{c}.step": torch.tensor(0.0)}
+    for (i, _, p, b) in entries:
+        shape = tuple(p.shape) if p.dim() > 0 else (1,)
+        for f in _FIELDS:
+            buf = torch.zeros(shape, dtype=torch.float32, device=b.master.device)
+            sd[f"{c}.p{i}.{f}"] = _sharded_param(buf, shape, b.buf.dp, b.buf.dp_rank, _group(b))
+    dcp.load(sd, checkpoint_id=path)
     optimizer.step_count = int(sd[f"{c}.step"].item())
     meta = torch.load(os.path.join(path, "nxd_param_groups.pt"), weights_only=True)
     for g, sg in zip(optimizer.param_groups, meta["param_groups"]):
         g.update(sg)
+    by_buf: Dict[int, Dict[int, Dict[str, torch.Tensor]]] = {}
+    for (i, _, p, b) in entries:
+        shape = tuple(p.shape) if p.dim() > 0 else (1,)
+        rows = {}
+        for f in _FIELDS:
+            st = sd[f"{c}.p{i}.{f}"]
+            lo, hi = _rows(shape[0], b.buf.dp, b.buf.dp_rank)
+            padded = torch.zeros((-(-shape[0] // b.buf.dp),) + shape[1:], dtype=torch.float32, device=b.master.device)
+            if hi > lo:
+                padded[:hi - lo].copy_(st.local_shards()[0].tensor)
+            rows[f] = padded
+        by_buf.setdefault(id(b), {})[id(p)] = rows
     for b in optimizer.buffers:
-        for (s, e, lo) in b.local:
-            b.buf.param_data[s:e].copy_(b.master[lo:lo + e - s])
-        b.buf.gather_params()
+        load_full_states(b, by_buf.get(id(b), {}), sharded=True)
+    optimizer._after_load()

@@ -161,10 +161,10 @@ class _FlatEPZero1(FlatMixedPrecisionAdamW):
     expert parameters over the expert-data-parallel group (their own flat buffers, gradients averaged
     over the whole DP world); ONE gradient norm over both (every shard counted once) clips both.
 
-    state_dict() has the reference's combined layout: the dense optimizer's entries first, the expert
-    optimizer's after them at `ep_param_id_offset` / `ep_param_group_offset` / `ep_base_state_offset`
-    / `ep_shape_info_offset`; `base_state` holds the flat fp32 master / moment shards of each buffer,
-    `shape_info` the parameter shapes, `state` the per-parameter step."""
+    state_dict() has the reference's combined layout (optimizer/zero_layout.py per part): the dense
+    optimizer's torch_xla ZeRO entries first, the expert optimizer's after them at
+    `ep_param_id_offset` / `ep_param_group_offset` / `ep_base_state_offset` / `ep_shape_info_offset`
+    (reference zero_redundancy_optimizer.py:281-362)."""
 
     def _split(self):
         dense = [b for b in self.buffers if not b.buf.name.endswith(":ep")]
@@ -172,59 +172,61 @@ class _FlatEPZero1(FlatMixedPrecisionAdamW):
         return dense, expert
 
     def state_dict(self) -> Dict[str, Any]:
-        flat = super().state_dict()
+        from .zero_layout import reference_state_dict
+
         dense, expert = self._split()
-        bufs = {id(b): sb for b, sb in zip(self.buffers, flat["buffers"])}
-        n_groups = len(flat["param_groups"])
+        d = reference_state_dict(self, dense)
+        e = reference_state_dict(self, expert)
 
-        def part(blist, pid0, bid0, goff):
-            state, base, shapes = {}, {}, {}
-            pid = pid0
-            for i, b in enumerate(blist):
-                sb = dict(bufs[id(b)])
-                sb["layout"] = [(gi + goff, pi, off, n, shp) for (gi, pi, off, n, shp) in sb["layout"]]
-                base[bid0 + i] = sb
-                for (_, _, _, _, shp) in sb["layout"]:
-                    shapes[pid] = shp
-                    state[pid] = {"step": flat["step"]}
-                    pid += 1
-            return state, base, shapes
+        def offset(dct):
+            return max(dct) + 1 if len(dct) > 0 else 1
 
-        d_state, d_base, d_shapes = part(dense, 0, 0, 0)
-        ep_pid = len(d_shapes)
-        e_state, e_base, e_shapes = part(expert, ep_pid, len(dense), n_groups)
-        return {
-            "ep_param_id_offset": max(ep_pid, 1) if not d_shapes else ep_pid,
-            "ep_param_group_offset": n_groups,
-            "ep_base_state_offset": len(dense),
-            "ep_shape_info_offset": ep_pid,
-            "param_groups": flat["param_groups"] + flat["param_groups"],
-            "state": {**d_state, **e_state},
-            "base_state": {**d_base, **e_base},
-            "shape_info": {**d_shapes, **e_shapes},
-            "step": flat["step"],
-            "zero1": flat["zero1"],
-        }
+        ep_pid, ep_base, ep_shape = offset(d["state"]), offset(d["base_state"]), offset(d["shape_info"])
+        out = {"ep_param_id_offset": ep_pid, "ep_param_group_offset": len(d["param_groups"]),
+               "ep_base_state_offset": ep_base, "ep_shape_info_offset": ep_shape,
+               "param_groups": d["param_groups"] + e["param_groups"],
+               "state": dict(d["state"]), "base_state": dict(d["base_state"]), "shape_info": dict(d["shape_info"]),
+               "sharded_master_weights": dict(d["sharded_master_weights"])}
+        for k, v in e["state"].items():
+            out["state"][ep_pid + k] = v
+        for k, v in e["base_state"].items():
+            out["base_state"][ep_base + k] = v
+            out["sharded_master_weights"][ep_base + k] = e["sharded_master_weights"][k]
+        for k, v in e["shape_info"].items():
+            out["shape_info"][ep_shape + k] = v
+        return out
 
     def load_state_dict(self, sd: Dict[str, Any]) -> None:
+        from .zero_layout import load_reference_state_dict
+
         if sd.get("flat_optimizer") or sd.get("flat_optimizer_full"):
             return super().load_state_dict(sd)
         keys = ("ep_param_id_offset", "ep_param_group_offset", "ep_base_state_offset", "ep_shape_info_offset")
         if any(k not in sd for k in keys):
             raise ValueError("state_dict is not compatible with expert parallelism and Zero-1.")
-        goff, boff = int(sd["ep_param_group_offset"]), int(sd["ep_base_state_offset"])
+        pid, goff = int(sd["ep_param_id_offset"]), int(sd["ep_param_group_offset"])
+        boff, soff = int(sd["ep_base_state_offset"]), int(sd["ep_shape_info_offset"])
+
+        def split(key, off):
+            lo, hi = {}, {}
+            for k, v in (sd.get(key) or {}).items():
+                (lo if k < off else hi)[k if k < off else k - off] = v
+            return lo, hi
+
+        st_d, st_e = split("state", pid)
+        bs_d, bs_e = split("base_state", boff)
+        sh_d, sh_e = split("shape_info", soff)
+        mw_d, mw_e = split("sharded_master_weights", boff)
         dense, expert = self._split()
-        base = sd["base_state"]
-        by_buf = {}
-        for i, b in enumerate(dense):
-            by_buf[id(b)] = base[i]
-        for i, b in enumerate(expert):
-            sb = dict(base[boff + i])
-            sb["layout"] = [(gi - goff, pi, off, n, shp) for (gi, pi, off, n, shp) in sb["layout"]]
-            by_buf[id(b)] = sb
-        flat = {"flat_optimizer": True, "step": int(sd["step"]), "param_groups": sd["param_groups"][:goff],
-                "buffers": [by_buf[id(b)] for b in self.buffers], "zero1": sd.get("zero1", True)}
-        super().load_state_dict(flat)
+        step = load_reference_state_dict(self, {"state": st_d, "base_state": bs_d, "shape_info": sh_d,
+                                                "sharded_master_weights": mw_d,
+                                                "param_groups": sd["param_groups"][:goff]}, dense)
+        if expert:
+            step = load_reference_state_dict(self, {"state": st_e, "base_state": bs_e, "shape_info": sh_e,
+                                                    "sharded_master_weights": mw_e,
+                                                    "param_groups": sd["param_groups"][goff:]}, expert)
+        self.step_count = step
+        self._after_load()
 
 
 def NeuronEPZero1Optimizer(params, optimizer_class=torch.optim.AdamW, grad_clipping: bool = True,

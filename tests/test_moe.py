@@ -228,7 +228,10 @@ def _w_mixtral_ckpt(rank, world, ep, ckpt_dir, resume, out):
             for k in ("ep_param_id_offset", "ep_param_group_offset", "ep_base_state_offset", "ep_shape_info_offset"):
                 assert k in sd, k
             assert len(sd["param_groups"]) == 2 * sd["ep_param_group_offset"]
-            assert all(b["name"].endswith(":ep") == (i >= sd["ep_base_state_offset"]) for i, b in sd["base_state"].items())
+            # torch_xla ZeRO entries: per-parameter shards, expert ones after the offset
+            assert all(set(v) == {"step", "exp_avg", "exp_avg_sq"} for v in sd["base_state"].values())
+            assert any(k >= sd["ep_base_state_offset"] for k in sd["base_state"])
+            assert set(sd["sharded_master_weights"]) == set(sd["base_state"])
     nxd.finalize_checkpoint()
     if rank == 0:
         torch.save(losses, out)
