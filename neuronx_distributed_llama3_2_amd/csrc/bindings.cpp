@@ -60,6 +60,7 @@ int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, i
 int wgrad_gemm_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int, int, int, int, hipStream_t);
 int wgrad_gemm_choose_splits(int, int, int);
 void wgrad_gemm_set_ablate(int);
+int cu_stream_launch(const void*, void*, int64_t, int, int64_t, hipStream_t);
 int moe_combine_fwd_launch(const void*, const int64_t*, const float*, void*, int64_t, int, int, hipStream_t);
 int moe_combine_bwd_launch(const void*, const void*, const int64_t*, const float*, void*, float*, int64_t, int, int,
                            hipStream_t);
@@ -847,6 +848,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("expert_gemv", &expert_gemv);
   m.def("grouped_gemm", &grouped_gemm);
   m.def("wgrad_gemm", &wgrad_gemm);
+  // diagnostics: copy kernel on exactly `blocks` workgroups (CU-interference measurements)
+  m.def("cu_stream", [](at::Tensor src, at::Tensor dst, int64_t bytes_per_block, int64_t blocks, int64_t ticks) {
+    check_cuda(src, "src");
+    check_cuda(dst, "dst");
+    TORCH_CHECK(src.is_contiguous() && dst.is_contiguous() && src.nbytes() == dst.nbytes(), "cu_stream: buffers");
+    TORCH_CHECK(bytes_per_block * blocks <= (int64_t)src.nbytes(), "cu_stream: buffers too small");
+    check_rc(nxd::cu_stream_launch(src.data_ptr(), dst.data_ptr(), bytes_per_block, (int)blocks, ticks, cur_stream()),
+             "cu_stream");
+  });
   m.def("wgrad_gemm_set_ablate", [](int64_t v) { nxd::wgrad_gemm_set_ablate((int)v); });
   m.def("wgrad_gemm_splits", [](int64_t T, int64_t M, int64_t N) { return nxd::wgrad_gemm_choose_splits((int)T, (int)M, (int)N); });
   m.def("moe_combine_fwd", &moe_combine_fwd);

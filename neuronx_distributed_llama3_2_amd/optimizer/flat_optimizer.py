@@ -25,6 +25,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..parallel import comm
 from ..parallel.grad_buffer import KIND_DUP, KIND_DUP_SP, KIND_SHARDED, FlatBuffer, find_shared_params, param_kind
 from ..parallel_layers import parallel_state as ps
 
@@ -165,15 +166,10 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
             b.buf.finish_grad_sync(average=True)
         tp_group, _ = self._tp()
         if tp_group is not None:
-            sp = [b.buf.grad_data for b in self.buffers if b.buf.kind == KIND_DUP_SP]
-            if sp:
-                flat = sp[0] if len(sp) == 1 else torch.cat(sp)
-                dist.all_reduce(flat, group=tp_group)
-                if len(sp) > 1:
-                    off = 0
-                    for g in sp:
-                        g.copy_(flat[off:off + g.numel()])
-                        off += g.numel()
+            # sequence-parallel norm-weight gradients: partial sums over TP (reference
+            # grads.py:313-329), all buffers in one coalesced all-reduce
+            comm.all_reduce_coalesced([b.buf.grad_data for b in self.buffers if b.buf.kind == KIND_DUP_SP],
+                                      group=tp_group)
 
     def _grad_norm_sq(self) -> torch.Tensor:
         tp_group, tp_rank = self._tp()

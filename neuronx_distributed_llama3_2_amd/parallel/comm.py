@@ -15,6 +15,15 @@ leaked-handle class of bugs that otherwise shows up as silent corruption or a ha
 The gloo backend (CPU test harness) lacks the "_base" flat-tensor collectives; the same calls are
 emulated there with list all-gathers / all-reduce + slice, so the parallel code paths are the same
 on CPU and GPU.
+
+Native RCCL layer (`NXD_NATIVE_COMM=1` or `set_native_comm(True)`): GPU tensors on an RCCL group go
+through parallel/native_comm.NativeCommunicator (csrc/comm.cpp) instead of the ProcessGroup: the
+DP bucket reduce-scatter / all-gather / all-reduce of parallel/grad_buffer.py and the coalesced
+sequence-parallel norm-gradient all-reduce (`all_reduce_coalesced`: one RCCL group launch for the
+list, no concatenation copy) run on the communicator's high-priority HIP stream, ordered by
+events.  One communicator per process group, created at the group's first collective (all its
+ranks get there together).  Off by default: torch's ProcessGroupNCCL is the path the multi-GPU
+bench has run; CPU / gloo tensors always take the torch path.
 """
 
 from __future__ import annotations
@@ -87,6 +96,38 @@ class _Done:
         return True
 
 
+_native = os.environ.get("NXD_NATIVE_COMM", "0") == "1"
+_native_comms: Dict[object, object] = {}
+
+
+def set_native_comm(enabled: bool) -> None:
+    global _native
+    _native = bool(enabled)
+
+
+def native_comm_enabled() -> bool:
+    return _native
+
+
+def _native_for(group, t: torch.Tensor):
+    """The native communicator for `group` when the native layer applies to tensor `t`."""
+    if not _native or not t.is_cuda or _is_gloo(group):
+        return None
+    key = group if group is not None else "world"
+    c = _native_comms.get(key)
+    if c is None:
+        from .native_comm import NativeCommunicator
+
+        c = _native_comms[key] = NativeCommunicator(group)
+    return c
+
+
+def _native_result(work, async_op: bool, op: str, t: torch.Tensor):
+    if not async_op:
+        return None
+    return _track(work if work is not None else _Done(), op, t)
+
+
 def _is_gloo(group) -> bool:
     try:
         return dist.get_backend(group) == "gloo"
@@ -96,6 +137,9 @@ def _is_gloo(group) -> bool:
 
 def all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
     """out[i*n:(i+1)*n] = inp of rank i (dim 0)."""
+    nc = _native_for(group, out)
+    if nc is not None:
+        return _native_result(nc.all_gather([out], [inp.contiguous()], async_op=async_op), async_op, "all_gather", out)
     if not _is_gloo(group):
         w = dist.all_gather_into_tensor(out, inp.contiguous(), group=group, async_op=async_op)
         return _track(w, "all_gather", out) if async_op else w
@@ -112,6 +156,10 @@ def all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, asy
 def reduce_scatter_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False,
                           op=dist.ReduceOp.SUM):
     """out = sum over ranks of inp[rank*n:(rank+1)*n] (dim 0)."""
+    nc = _native_for(group, inp) if op == dist.ReduceOp.SUM else None
+    if nc is not None:
+        w = nc.reduce_scatter([out], [inp.contiguous()], "sum", async_op=async_op)
+        return _native_result(w, async_op, "reduce_scatter", inp)
     if not _is_gloo(group):
         w = dist.reduce_scatter_tensor(out, inp.contiguous(), op=op, group=group, async_op=async_op)
         return _track(w, "reduce_scatter", inp) if async_op else w
@@ -124,8 +172,32 @@ def reduce_scatter_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, asyn
 
 
 def all_reduce(t: torch.Tensor, group=None, async_op: bool = False, op=dist.ReduceOp.SUM):
+    nc = _native_for(group, t) if op == dist.ReduceOp.SUM and t.is_contiguous() else None
+    if nc is not None:
+        return _native_result(nc.all_reduce([t], "sum", async_op=async_op), async_op, "all_reduce", t)
     w = dist.all_reduce(t, op=op, group=group, async_op=async_op)
     return _track(w, "all_reduce", t) if async_op else w
+
+
+def all_reduce_coalesced(tensors: List[torch.Tensor], group=None) -> None:
+    """In-place sum of every tensor over `group`: one RCCL group launch on the native layer, else
+    one all-reduce of their concatenation (copied back)."""
+    tensors = [t for t in tensors if t.numel()]
+    if not tensors or dist.get_world_size(group=group) == 1:
+        return
+    nc = _native_for(group, tensors[0]) if all(t.is_contiguous() for t in tensors) else None
+    if nc is not None:
+        nc.all_reduce(list(tensors), "sum", async_op=False)
+        return
+    if len(tensors) == 1:
+        dist.all_reduce(tensors[0], group=group)
+        return
+    flat = torch.cat([t.reshape(-1) for t in tensors])
+    dist.all_reduce(flat, group=group)
+    off = 0
+    for t in tensors:
+        t.copy_(flat[off:off + t.numel()].view_as(t))
+        off += t.numel()
 
 
 def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):

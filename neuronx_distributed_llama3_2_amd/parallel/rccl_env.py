@@ -6,9 +6,16 @@ knob that matters is how many channels (= RCCL workgroups, i.e. CUs taken from c
 collective uses.  The chunked SP overlap (parallel_layers/sp.py) wants collectives that leave
 most CUs to the concurrent GEMM; a pure comm benchmark wants many channels.  Both are settable:
 
-    NXD_RCCL_CHANNELS=<n>   -> NCCL_MIN_NCHANNELS = NCCL_MAX_NCHANNELS = n   (unset: RCCL picks)
+    NXD_RCCL_CHANNELS=<n>   -> NCCL_MAX_NCHANNELS = n (default 16; 0 / "auto": RCCL picks)
     NXD_COMM_HIGH_PRIORITY  -> TP / EP groups get high-priority RCCL streams (default 1;
                                parallel_layers/parallel_state.py)
+
+Default channel cap, from profiles/r3_cu_interference.jsonl (one MI355X: TP=8-shape GEMMs and the
+FA forward on the compute stream while a copy kernel of K workgroups -- RCCL runs one per channel --
+streams on a side stream): any concurrent side kernel costs 12-30 % at K = 4-16 (flat), rising to
+1.4-2.4x at K = 64-128.  A ring channel moves about one xGMI link's worth, so 16 channels (> 2 per
+link of the 7) keep the links busy while staying on the flat part of that curve for the SP
+all-gathers / reduce-scatters that overlap GEMMs.  Only the cap is set (RCCL may use fewer).
 
 `apply_rccl_env()` sets library defaults BEFORE `init_process_group` without overriding anything
 the user exported; `log_comm_config()` logs the effective RCCL-related environment once per
@@ -33,6 +40,8 @@ RCCL_DEFAULTS: Dict[str, str] = {
     "TORCH_NCCL_AVOID_RECORD_STREAMS": "1",
 }
 
+DEFAULT_CHANNELS = 16
+
 _PREFIXES = ("NCCL_", "RCCL_", "TORCH_NCCL_", "NXD_RCCL", "NXD_COMM", "NXD_SP_CHUNKS", "HSA_ENABLE_IPC")
 _logged = False
 
@@ -41,9 +50,8 @@ def apply_rccl_env(extra: Optional[Dict[str, str]] = None) -> Dict[str, str]:
     """Set the library's RCCL defaults (and `extra`) where the environment does not already
     define them.  Returns what was set.  Call before `torch.distributed.init_process_group`."""
     want = dict(RCCL_DEFAULTS)
-    ch = os.environ.get("NXD_RCCL_CHANNELS")
-    if ch:
-        want["NCCL_MIN_NCHANNELS"] = ch
+    ch = os.environ.get("NXD_RCCL_CHANNELS", str(DEFAULT_CHANNELS))
+    if ch and ch not in ("0", "auto"):
         want["NCCL_MAX_NCHANNELS"] = ch
     if extra:
         want.update(extra)

@@ -20,7 +20,7 @@ def test_bench_collectives_gloo():
     assert {x["op"] for x in recs} == {"all_gather", "reduce_scatter", "all_reduce", "p2p_neighbours"}
     for x in recs:
         assert x["ranks"] == 3 and x["busbw_gbs"] > 0
-        assert x["env"]["NCCL_MIN_NCHANNELS"] == "16" and x["env"]["NCCL_MAX_NCHANNELS"] == "16"
+        assert x["env"]["NCCL_MAX_NCHANNELS"] == "16"
 
 
 def test_apply_rccl_env_respects_user(monkeypatch):
@@ -35,3 +35,22 @@ def test_apply_rccl_env_respects_user(monkeypatch):
     assert cfg["TORCH_NCCL_AVOID_RECORD_STREAMS"] == "0"
     if "NCCL_DEBUG" in applied:
         monkeypatch.delenv("NCCL_DEBUG")
+
+
+def test_default_channel_cap_logged(monkeypatch):
+    """The measured default (16 channels max, profiles/r3_cu_interference.jsonl) is applied unless the
+    user set NCCL_MAX_NCHANNELS or NXD_RCCL_CHANNELS=auto, and appears in the logged config."""
+    from neuronx_distributed_llama3_2_amd.parallel import rccl_env
+
+    monkeypatch.delenv("NXD_RCCL_CHANNELS", raising=False)
+    monkeypatch.delenv("NCCL_MAX_NCHANNELS", raising=False)
+    applied = rccl_env.apply_rccl_env()
+    assert applied.get("NCCL_MAX_NCHANNELS") == str(rccl_env.DEFAULT_CHANNELS)
+    assert rccl_env.log_comm_config(force=True)["NCCL_MAX_NCHANNELS"] == "16"
+    monkeypatch.delenv("NCCL_MAX_NCHANNELS")
+    monkeypatch.setenv("NXD_RCCL_CHANNELS", "auto")
+    assert "NCCL_MAX_NCHANNELS" not in rccl_env.apply_rccl_env()
+    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "40")
+    monkeypatch.delenv("NXD_RCCL_CHANNELS")
+    rccl_env.apply_rccl_env()
+    assert os.environ["NCCL_MAX_NCHANNELS"] == "40"

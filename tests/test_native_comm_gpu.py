@@ -57,3 +57,28 @@ def test_native_comm_single_rank_semantics():
         assert float(big[-1]) == 3.0
     finally:
         c.close()
+
+
+def test_comm_layer_routes_gpu_tensors_to_native_rccl():
+    """NXD_NATIVE_COMM on: the framework's comm primitives (used by the DP grad buckets and the SP
+    norm-gradient all-reduce) run on the native communicator for RCCL-group GPU tensors."""
+    _comm()
+    from neuronx_distributed_llama3_2_amd.parallel import comm
+
+    comm.set_native_comm(True)
+    try:
+        x = torch.randn(1024, device="cuda")
+        ref = x.clone()
+        w = comm.all_reduce(x, async_op=True)
+        w.wait()
+        assert torch.equal(x, ref)
+        out = torch.empty(1024, device="cuda")
+        comm.reduce_scatter_tensor(out, x, async_op=True).wait()
+        assert torch.equal(out, ref)
+        g = torch.empty(1024, device="cuda")
+        comm.all_gather_into_tensor(g, out)
+        torch.cuda.synchronize()
+        assert torch.equal(g, ref)
+        assert len(comm._native_comms) == 1      # one communicator for the world group
+    finally:
+        comm.set_native_comm(False)
