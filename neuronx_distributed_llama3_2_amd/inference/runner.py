@@ -86,6 +86,19 @@ class InferenceRunner:
                 tok.save_pretrained(traced_model_path)
 
     def load_neuron_model(self, traced_model_path: str):
+        """In-process model; a traced model with tp_degree > 1 loaded without torch.distributed
+        (plain `python`, no launcher) is served by resident per-GPU workers instead
+        (inference/spmd_server.py: one controller, ids in / ids out)."""
+        import torch.distributed as dist
+
+        cfg = InferenceConfig.from_pretrained(traced_model_path)
+        if int(cfg.tp_degree) > 1 and not dist.is_initialized():
+            from .spmd_server import SpmdGenerationServer
+
+            app = "llama" if self.app_cls is LlamaForCausalLMInference else self.app_cls.__name__
+            m = SpmdGenerationServer.from_compiled(traced_model_path, int(cfg.tp_degree), app=app)
+            self.config = m.config
+            return m
         m = self.app_cls.load(traced_model_path)
         self.config = m.config
         return m

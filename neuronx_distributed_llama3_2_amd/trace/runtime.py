@@ -76,6 +76,16 @@ class _SharedSlots:
         return [b[:math.prod(shape)].view(shape) for b, shape in zip(self.bufs, meta)]
 
 
+def _tensor_bytes(x) -> int:
+    if isinstance(x, torch.Tensor):
+        return x.numel() * x.element_size()
+    if isinstance(x, (list, tuple)):
+        return sum(_tensor_bytes(v) for v in x)
+    if isinstance(x, dict):
+        return sum(_tensor_bytes(v) for v in x.values())
+    return 0
+
+
 def _flatten_out(out):
     """(tensors, structure) of a forward's output: a tensor or a (nested) list / tuple of them."""
     if isinstance(out, torch.Tensor):
@@ -153,9 +163,10 @@ def _worker_main(rank, world, port, build_fn, build_args, cmd_q, res_q):
             elif cmd == "forward":
                 out = obj(*_to_dev(payload, dev))
                 res_q.put(("ok", rank, _to_host(out) if rank == 0 else None))
-            elif cmd == "call":      # (method name, args): e.g. save
-                name, args = payload
-                r = getattr(obj, name)(*args)
+            elif cmd == "call":      # (method name, args[, kwargs]): e.g. save, generate
+                name, args = payload[0], payload[1]
+                kwargs = payload[2] if len(payload) > 2 else {}
+                r = getattr(obj, name)(*_to_dev(args, dev), **kwargs)
                 res_q.put(("ok", rank, _to_host(r) if rank == 0 else None))
         except Exception:
             res_q.put(("err", rank, traceback.format_exc()))
@@ -166,6 +177,8 @@ def _worker_main(rank, world, port, build_fn, build_args, cmd_q, res_q):
 
 
 class SpmdWorkerPool:
+    last_host_bytes = 0
+
     def __init__(self, world: int, build_fn: Callable, build_args: Sequence[Any] = (), timeout: float = 1800.0):
         ctx = mp.get_context("spawn")
         self.world, self.timeout = world, timeout
@@ -220,10 +233,15 @@ class SpmdWorkerPool:
 
     __call__ = forward
 
-    def call(self, name: str, *args):
+    def call(self, name: str, *args, **kwargs):
+        """Run `obj.<name>(*args, **kwargs)` on every rank (tensors moved to each rank's device);
+        rank 0's result comes back.  `last_host_bytes` counts the tensor bytes this call moved
+        between the controller and the workers."""
         for q in self.cmd_q:
-            q.put(("call", (name, args)))
-        return self._collect()
+            q.put(("call", (name, args, kwargs)))
+        r = self._collect()
+        self.last_host_bytes = self.world * _tensor_bytes(args) + _tensor_bytes(kwargs) * self.world + _tensor_bytes(r)
+        return r
 
     def close(self) -> None:
         for q in self.cmd_q:

@@ -296,3 +296,31 @@ def test_gqa_convert_to_mha_matches_hf_and_tp1():
     a, b = torch.load(os.path.join(d, "a.pt")), torch.load(os.path.join(d, "b.pt"))
     assert torch.equal(a["out"], b["out"])
     assert torch.equal(a["out"][:, 12], a["ref_next"])
+
+
+def test_spmd_generation_server_tp2_resident_o_tokens():
+    """Resident TP=2 generation through the single-controller worker pool: matches in-process TP=1,
+    and the controller <-> worker traffic of a call is the token ids only (O(tokens))."""
+    from neuronx_distributed_llama3_2_amd.inference.spmd_server import SpmdGenerationServer
+    from neuronx_distributed_llama3_2_amd.models.llama.convert import hf_to_nxd
+
+    cfg = _tiny_cfg()
+    hf = _hf_model(cfg, seed=6)
+    full = hf_to_nxd(hf.state_dict(), cfg)
+    d = tempfile.mkdtemp()
+    path = os.path.join(d, "full.pt")
+    torch.save(full, path)
+    torch.manual_seed(5)
+    ids = torch.randint(3, cfg.vocab_size, (2, 9))
+    ref = _inf_model(cfg, hf.state_dict()).generate(ids, max_new_tokens=8, eos_token_id=-1)
+    kw = dict(batch_size=2, seq_len=64, max_context_length=32)
+    with SpmdGenerationServer.from_full_state_dict(cfg.to_dict(), path, 2, kw, dtype="float32") as srv:
+        out = srv.generate(ids, max_new_tokens=8, eos_token_id=-1)
+        b8 = srv.last_host_bytes
+        out16 = srv.generate(ids, max_new_tokens=16, eos_token_id=-1)
+        b16 = srv.last_host_bytes
+    assert torch.equal(out, ref)
+    assert torch.equal(out16[:, :17], ref)
+    # ids in (to each of 2 ranks) + ids out, int64: no activations / logits cross processes
+    assert b8 == 8 * (2 * ids.numel() + out.numel()), b8
+    assert b16 - b8 == 8 * 2 * 8     # 8 more tokens for each of 2 sequences
