@@ -6,7 +6,10 @@ GPU (torchrun or Lightning's own subprocess launcher) that initialises the NxD p
 framework's flat-buffer optimizer (no DDP wrapper), and checkpoints through the NxD sharded
 checkpoint API.  Lightning is an optional dependency: `lightning` (2.x) or `pytorch_lightning`
 must be importable; it is NOT installed in this build environment, so these classes are written
-against its public API and import-gated (parity unpinned by tests here).
+against its public API and import-gated.  tests/test_lightning_examples.py drives them (and the
+examples under examples/training/llama/lightning/) on gloo ranks through a stand-in of that API
+(tests/fake_lightning.py): the Lightning-driven run equals the training-API run step for step;
+behaviour against real Lightning stays unpinned.
 """
 
 from ._compat import HAVE_LIGHTNING, require_lightning  # noqa: F401

@@ -7,6 +7,7 @@ import torch
 
 from ..parallel_layers import parallel_state as ps
 from ..trainer import initialize_parallel_model, initialize_parallel_optimizer
+from ..trainer.optimizer import NxDOptimizer
 from ..utils.training_utils import get_param_groups_by_weight_decay
 from ._compat import pl, require_lightning
 
@@ -51,7 +52,8 @@ class NeuronLTModule(pl.LightningModule):
 
     def training_step(self, batch, batch_idx):
         opt = self.optimizers()
-        opt = getattr(opt, "optimizer", opt)
+        while not isinstance(opt, NxDOptimizer) and hasattr(opt, "optimizer"):   # LightningOptimizer wrapper
+            opt = opt.optimizer
         pp = ps.get_pipeline_model_parallel_size() > 1
         if pp:
             loss = self.model.run_train(**batch)

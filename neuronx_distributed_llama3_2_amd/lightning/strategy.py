@@ -19,8 +19,8 @@ class NeuronXLAStrategy(DDPStrategy):
     def __init__(self, nxd_config: Optional[Dict[str, Any]] = None, tensor_parallel_size: int = 1,
                  pipeline_parallel_size: int = 1, expert_parallel_size: int = 1, debug: bool = False,
                  sync_module_states: bool = False, checkpoint_io: Optional[NeuronCheckpointIO] = None,
-                 save_load_xser: bool = True, **kwargs):
-        super().__init__(process_group_backend="nccl", checkpoint_io=checkpoint_io or
+                 save_load_xser: bool = True, process_group_backend: str = "nccl", **kwargs):
+        super().__init__(process_group_backend=process_group_backend, checkpoint_io=checkpoint_io or
                          NeuronCheckpointIO(save_load_xser=save_load_xser), **kwargs)
         self.nxd_config = nxd_config
         if nxd_config is not None:

@@ -233,10 +233,9 @@ def _w_finetune(rank, world, hf_dir, data, out_dir, tp):
         torch.save((before, after), os.path.join(out_dir, f"ft_{tp}.pt"))
 
 
-def test_llama_instruction_finetune_example(tmp_path):
-    """examples/training/llama/tp_llama_hf_finetune.py (reference E3 fine-tuning path): HF Llama
-    checkpoint + tokenizer -> TP shard -> packed Dolly-style data -> response loss drops; the
-    pre-training response loss is the same at TP1 and TP2 (HF->NxD conversion + sharding)."""
+def _finetune_fixture(tmp_path):
+    """Tiny HF Llama checkpoint + word-level tokenizer + Dolly-style JSONL (shared with the
+    Lightning fine-tune test)."""
     from tokenizers import Tokenizer, models, pre_tokenizers
     from transformers import LlamaConfig, LlamaForCausalLM, PreTrainedTokenizerFast
 
@@ -263,6 +262,14 @@ def test_llama_instruction_finetune_example(tmp_path):
         for _ in range(6):
             for q, ans in facts:
                 f.write(json.dumps({"instruction": q, "context": "", "response": ans}) + "\n")
+    return hf_dir, data
+
+
+def test_llama_instruction_finetune_example(tmp_path):
+    """examples/training/llama/tp_llama_hf_finetune.py (reference E3 fine-tuning path): HF Llama
+    checkpoint + tokenizer -> TP shard -> packed Dolly-style data -> response loss drops; the
+    pre-training response loss is the same at TP1 and TP2 (HF->NxD conversion + sharding)."""
+    hf_dir, data = _finetune_fixture(tmp_path)
     run_distributed(_w_finetune, 2, hf_dir, data, str(tmp_path / "tp2"), 2)
     run_distributed(_w_finetune, 1, hf_dir, data, str(tmp_path / "tp1"), 1)
     b2, a2 = torch.load(tmp_path / "tp2" / "ft_2.pt")
