@@ -6,16 +6,19 @@
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
+#include "common.h"
+
 namespace nxd {
 int flash_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, const int64_t*,
-                          const int64_t*, const int64_t*, int, int, int, int, int, int, float, int, int, hipStream_t);
+                          const int64_t*, const int64_t*, int, int, int, int, int, int, float, int, int,
+                          const DropoutArgs&, hipStream_t);
 int64_t flash_attn_bwd_workspace(int, int, int, int, int, int);
 void flash_attn_bwd_set_knob(int, int);
 int transpose_bf16_launch(const void*, void*, int64_t, int64_t, int64_t, int64_t, hipStream_t);
 int flash_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*, float*,
                           void*, void*, void*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                           const int64_t*, const int64_t*, const int64_t*, const int64_t*, int, int, int, int, int, int,
-                          float, int, int, hipStream_t);
+                          float, int, int, const DropoutArgs&, hipStream_t);
 int rmsnorm_fwd_launch(const void*, const void*, const void*, void*, void*, float*, int64_t, int, float, hipStream_t);
 int rmsnorm_bwd_num_partials(int64_t);
 int rmsnorm_bwd_launch(const void*, const void*, const void*, const float*, const void*, void*, float*, float*, int,
@@ -95,8 +98,19 @@ void bshd_strides(const at::Tensor& t, const char* n, int64_t* s) {
   s[2] = t.stride(2);
 }
 
+// dropout_p in [0, 1): keep iff hash >= p * 2^32 (truncated, as ops/attention_dropout.py), scale 1/(1-p)
+nxd::DropoutArgs dropout_args(double p, int64_t seed, int64_t head_offset) {
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout_p must be in [0, 1)");
+  nxd::DropoutArgs d;
+  d.thresh = (uint32_t)(uint64_t)(p * 4294967296.0);
+  d.scale = (float)(1.0 / (1.0 - p));
+  d.seed = (uint32_t)(seed & 0xFFFFFFFFll);
+  d.head_offset = (int)head_offset;
+  return d;
+}
+
 void flash_attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse, double scale, bool causal,
-                    int64_t causal_offset) {
+                    int64_t causal_offset, double dropout_p, int64_t seed, int64_t head_offset) {
   int64_t qs[3], ks[3], vs[3], os[3];
   bshd_strides(q, "q", qs);
   bshd_strides(k, "k", ks);
@@ -113,12 +127,13 @@ void flash_attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::
               "lse must be contiguous fp32 [B, Hq, Sq]");
   check_rc(nxd::flash_attn_fwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), qs, ks,
                                       vs, os, B, Sq, Sk, Hq, Hkv, D, (float)scale, causal ? 1 : 0, (int)causal_offset,
-                                      cur_stream()),
+                                      dropout_args(dropout_p, seed, head_offset), cur_stream()),
            "flash_attn_fwd");
 }
 
 void flash_attn_bwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor dout, at::Tensor lse,
-                    at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t causal_offset) {
+                    at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t causal_offset,
+                    double dropout_p, int64_t seed, int64_t head_offset) {
   int64_t qs[3], ks[3], vs[3], os[3], dos[3], dqs[3], dks[3], dvs[3];
   bshd_strides(q, "q", qs);
   bshd_strides(k, "k", ks);
@@ -142,7 +157,8 @@ void flash_attn_bwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::
   check_rc(nxd::flash_attn_bwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                                       lse.data_ptr<float>(), ws.data_ptr<float>(), dq.data_ptr(),
                                       dk.data_ptr(), dv.data_ptr(), qs, ks, vs, os, dos, dqs, dks, dvs, B, Sq, Sk, Hq, Hkv, D,
-                                      (float)scale, causal ? 1 : 0, (int)causal_offset, cur_stream()),
+                                      (float)scale, causal ? 1 : 0, (int)causal_offset,
+                                      dropout_args(dropout_p, seed, head_offset), cur_stream()),
            "flash_attn_bwd");
 }
 
@@ -868,8 +884,12 @@ PYBIND11_MODULE(_C, m) {
     else nxd::dgemv_set_knob(which, value);
   });
   m.doc() = "CDNA4 (gfx950) kernels of neuronx_distributed_llama3_2_amd";
-  m.def("flash_attn_fwd", &flash_attn_fwd);
-  m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("flash_attn_fwd", &flash_attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"),
+        py::arg("scale"), py::arg("causal"), py::arg("causal_offset"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0,
+        py::arg("head_offset") = 0);
+  m.def("flash_attn_bwd", &flash_attn_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"),
+        py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"), py::arg("causal"),
+        py::arg("causal_offset"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("head_offset") = 0);
   // A/B knobs of the backward: 0 = ablation flags, 1 = chunk override (0 = auto)
   m.def("flash_attn_set_knob", [](int which, int value) { nxd::flash_attn_bwd_set_knob(which, value); });
   m.def("rmsnorm_fwd", &rmsnorm_fwd);

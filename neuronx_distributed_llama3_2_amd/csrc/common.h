@@ -90,6 +90,31 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// Attention-dropout keep mask: a counter hash of (seed, batch, global head, query, key), so nothing
+// is stored and the backward regenerates the forward's mask.  Same definition as the host
+// reference ops/attention_dropout.py:dropout_keep_mask (keep iff hash >= p * 2^32).
+__host__ __device__ __forceinline__ uint32_t drop_hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  return x ^ (x >> 16);
+}
+__device__ __forceinline__ uint32_t drop_row_hash(uint32_t seed, int b, int head, int q) {
+  const uint32_t x = drop_hash32(seed ^ ((uint32_t)b * 0x9E3779B1u) ^ ((uint32_t)head * 0x85EBCA6Bu));
+  return drop_hash32(x ^ ((uint32_t)q * 0xC2B2AE35u));
+}
+__device__ __forceinline__ bool drop_keep(uint32_t row_hash, int key, uint32_t thresh) {
+  return drop_hash32(row_hash ^ ((uint32_t)key * 0x27D4EB2Fu)) >= thresh;
+}
+struct DropoutArgs {
+  uint32_t thresh = 0;      // keep iff hash >= thresh (= p * 2^32)
+  float scale = 1.f;        // 1 / (1 - p)
+  uint32_t seed = 0;
+  int head_offset = 0;      // global index of local head 0 (tensor-parallel ranks draw the global masks)
+  bool enabled() const { return thresh != 0; }
+};
+
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 inline int64_t ceil_div64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

@@ -69,6 +69,7 @@ struct BwdParams {
   int ablate;  // timing-only ablations (NXD_FAB_ABLATE; outputs wrong): 1 no dQ atomics,
                // 2 no dK/dV atomics, 16 no Q/dO tile loads,
                // 32 no per-tile barriers
+  DropoutArgs drop;  // DROP variants only
 };
 
 // (q head x q tile) iterations of key block kb
@@ -137,8 +138,11 @@ __device__ __forceinline__ void mfma_acc_agpr(f32x16_t& acc, const TA& a, const 
 }
 
 // PIPE: S / dP operand reads issued this many steps ahead of their MFMAs; PIPE_DVDK: the same for
-// the dV / dK transposed reads (the first ones go out before the softmax VALU)
-template <int D, int PIPE, int PIPE_DVDK>
+// the dV / dK transposed reads (the first ones go out before the softmax VALU).
+// DROP: attention dropout (reference NKI flash_attn_bwd dropout_p / seed): the forward's keep mask m
+// (0 or 1/(1-p)) is regenerated from the hash; dV uses P*m, dS = P * (m * dO.V^T - delta), so dP
+// starts at 0 instead of -delta and delta is re-read from the tile's LDS row constants.
+template <int D, int PIPE, int PIPE_DVDK, bool DROP>
 __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
   constexpr int kPipe = PIPE;
   constexpr int CH = D / 8;
@@ -381,7 +385,7 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             s_acc[4 * gq + i] = l4[i];
-            dp_acc[4 * gq + i] = d4[i];
+            dp_acc[4 * gq + i] = DROP ? 0.f : d4[i];
           }
         }
         // operands of step s are read kPipe steps ahead of its MFMAs (explicit software pipeline:
@@ -435,10 +439,26 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
           }
         };
         auto p_half = [&](int h) {  // bf16 P / dS of half h, dS^T rows -> LDS
+          if constexpr (DROP) {
+            const f32x4_t nd0 = lds_ld<f32x4_t>(a_ld + LB + 128 + 32 * (2 * h));
+            const f32x4_t nd1 = lds_ld<f32x4_t>(a_ld + LB + 128 + 32 * (2 * h + 1));
+            const int my_key = kc0 + r;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            pf[h][j] = (__bf16)pv[8 * h + j];
-            dsf[h][j] = (__bf16)(pv[8 * h + j] * dp_acc[8 * h + j]);
+            for (int j = 0; j < 8; ++j) {
+              const int e = 8 * h + j;
+              const int qg = qt0 + 8 * (e >> 2) + 4 * hh + (e & 3);
+              const uint32_t rh = drop_row_hash(p.drop.seed, b, hq + p.drop.head_offset, qg);
+              const float m = drop_keep(rh, my_key, p.drop.thresh) ? p.drop.scale : 0.f;
+              const float nd = j < 4 ? nd0[j] : nd1[j - 4];
+              pf[h][j] = (__bf16)(pv[e] * m);
+              dsf[h][j] = (__bf16)(pv[e] * __builtin_fmaf(m, dp_acc[e], nd));
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              pf[h][j] = (__bf16)pv[8 * h + j];
+              dsf[h][j] = (__bf16)(pv[8 * h + j] * dp_acc[8 * h + j]);
+            }
           }
           // whole-vector bit casts (per-element extraction of bf16 ext_vectors miscompiles on ROCm 7.2)
           const u32x4_t dw = __builtin_bit_cast(u32x4_t, dsf[h]);
@@ -740,14 +760,15 @@ int pipe_variant() {
   return g_pipe;
 }
 
-template <int D, int PIPE, int PIPE_DVDK>
+template <int D, int PIPE, int PIPE_DVDK, bool DROP = false>
 void launch_bwd(const BwdParams& p, int64_t items, size_t lds, hipStream_t stream) {
   static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per instantiation
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)bwd_kernel<D, PIPE, PIPE_DVDK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)bwd_kernel<D, PIPE, PIPE_DVDK, DROP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((bwd_kernel<D, PIPE, PIPE_DVDK>), dim3((unsigned)items), dim3(kThreads), lds, stream, p);
+  hipLaunchKernelGGL((bwd_kernel<D, PIPE, PIPE_DVDK, DROP>), dim3((unsigned)items), dim3(kThreads), lds, stream, p);
 }
 
 }  // namespace fab
@@ -771,7 +792,7 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
                           const int64_t* qs, const int64_t* ks, const int64_t* vs, const int64_t* os,
                           const int64_t* dos, const int64_t* dqs, const int64_t* dks, const int64_t* dvs,
                           int B, int Sq, int Sk, int Hq, int Hkv, int D, float softmax_scale, int causal,
-                          int causal_offset, hipStream_t stream) {
+                          int causal_offset, const DropoutArgs& drop, hipStream_t stream) {
   using namespace fab;
   if (Hkv <= 0 || Hq % Hkv != 0 || (D != 64 && D != 128)) return -1;
   const int G = Hq / Hkv;
@@ -815,10 +836,13 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   items *= (int64_t)B * Hkv;
   p.ablate = ablate_flags();
   p.xcd_map = xcd_map_mode();
+  p.drop = drop;
   if (items > 0) {
     if (D == 128) {
       const size_t lds = kBlockK * 128 * 2 + 4 * kBlockQ * 128 * 2 + kBlockK * 64 + 512 + 128 * 128 * 2;
-      switch (pipe_variant()) {
+      if (drop.enabled()) {
+        launch_bwd<128, 1, 2, true>(p, items, lds, stream);
+      } else switch (pipe_variant()) {
         case 11: launch_bwd<128, 1, 1>(p, items, lds, stream); break;
         case 21: launch_bwd<128, 2, 1>(p, items, lds, stream); break;
         case 0: launch_bwd<128, 0, 0>(p, items, lds, stream); break;
@@ -826,7 +850,10 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
       }
     } else {
       const size_t lds = kBlockK * 64 * 2 + 4 * kBlockQ * 64 * 2 + kBlockK * 64 + 512 + 2 * 64 * 16 * 4 + 128 * 64 * 2;
-      launch_bwd<64, 1, 2>(p, items, lds, stream);
+      if (drop.enabled())
+        launch_bwd<64, 1, 2, true>(p, items, lds, stream);
+      else
+        launch_bwd<64, 1, 2>(p, items, lds, stream);
     }
   }
   if (D == 128) {

@@ -45,6 +45,7 @@ struct FwdParams {
   float scale_log2;  // softmax_scale * log2(e)
   int causal;
   int causal_offset;  // query i attends keys <= i + causal_offset (Sk - Sq for bottom-right alignment)
+  DropoutArgs drop;   // DROP variants only
 };
 
 // 16-byte chunk swizzle of a [rows][D] bf16 LDS image (D/8 chunks per row).
@@ -90,7 +91,10 @@ __device__ __forceinline__ float xor32(float x, bool is_max) {
 }
 
 // Double-buffered LDS ring of 64-key tiles: tile t + 1 is DMA'd while tile t is computed.
-template <int D, int W>
+// DROP: dropout on the probabilities (reference NKI flash_fwd dropout_p / seed): the row sum l and
+// the LSE use the undropped P, the P.V operand is P * keep / (1 - p); the lane's query row hash is
+// computed once, each score costs one more hash.
+template <int D, int W, bool DROP>
 __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
   constexpr int kWaves = W;
   constexpr int kBlockM = W * 32;                 // q rows per workgroup
@@ -146,6 +150,8 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
 #pragma unroll
   for (int i = 0; i < NDB; ++i) acc_o[i] = f32x16_t{0};
   float m_i = -INFINITY, l_i = 0.f;
+  uint32_t drow = 0;
+  if constexpr (DROP) drow = drop_row_hash(p.drop.seed, b, hq + p.drop.head_offset, my_q);
 
   // K/V tiles go global -> LDS directly (global_load_lds_dwordx4, 1 KiB per wave-instruction).
   // The LDS image is lane-linear per instruction, so the XOR swizzle is applied to the per-lane
@@ -280,7 +286,12 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
             for (int e = 0; e < 8; ++e) {
               const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j][8 * s2 + e], p.scale_log2, -m_use));
               rsum += pv;
-              pf[j][s2][e] = (__bf16)pv;
+              if constexpr (DROP) {
+                const int key = kt0 + 32 * j + (e & 3) + 8 * (2 * s2 + (e >> 2)) + 4 * hh;
+                pf[j][s2][e] = (__bf16)(drop_keep(drow, key, p.drop.thresh) ? pv * p.drop.scale : 0.f);
+              } else {
+                pf[j][s2][e] = (__bf16)pv;
+              }
             }
           }
         }
@@ -341,7 +352,7 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
 int flash_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse,
                           const int64_t* qs, const int64_t* ks, const int64_t* vs, const int64_t* os,
                           int B, int Sq, int Sk, int Hq, int Hkv, int D, float softmax_scale,
-                          int causal, int causal_offset, hipStream_t stream) {
+                          int causal, int causal_offset, const DropoutArgs& drop, hipStream_t stream) {
   using namespace fa;
   FwdParams p;
   p.q = (const uint16_t*)q;
@@ -357,6 +368,7 @@ int flash_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, 
   p.scale_log2 = softmax_scale * 1.4426950408889634f;
   p.causal = causal;
   p.causal_offset = causal_offset;
+  p.drop = drop;
   if (Hkv <= 0 || Hq % Hkv != 0) return -1;
   if (D != 128 && D != 64) return -2;
   // 8-wave workgroups (256 query rows: half the K/V tile traffic and barriers per row) while the
@@ -369,11 +381,17 @@ int flash_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, 
   const int grid = ((Sq + rows - 1) / rows) * B * Hq;
   if (grid == 0) return 0;
   const size_t lds = 2 * 2 * kBlockN * D * 2;
-#define NXD_FA_LAUNCH(DD, WW) hipLaunchKernelGGL((fwd_kernel<DD, WW>), dim3(grid), dim3(WW * 64), lds, stream, p)
-  if (D == 128) {
-    if (w8) NXD_FA_LAUNCH(128, 8); else NXD_FA_LAUNCH(128, 4);
+#define NXD_FA_LAUNCH(DD, WW, DR) hipLaunchKernelGGL((fwd_kernel<DD, WW, DR>), dim3(grid), dim3(WW * 64), lds, stream, p)
+  if (drop.enabled()) {
+    if (D == 128) {
+      if (w8) NXD_FA_LAUNCH(128, 8, true); else NXD_FA_LAUNCH(128, 4, true);
+    } else {
+      if (w8) NXD_FA_LAUNCH(64, 8, true); else NXD_FA_LAUNCH(64, 4, true);
+    }
+  } else if (D == 128) {
+    if (w8) NXD_FA_LAUNCH(128, 8, false); else NXD_FA_LAUNCH(128, 4, false);
   } else {
-    if (w8) NXD_FA_LAUNCH(64, 8); else NXD_FA_LAUNCH(64, 4);
+    if (w8) NXD_FA_LAUNCH(64, 8, false); else NXD_FA_LAUNCH(64, 4, false);
   }
 #undef NXD_FA_LAUNCH
   return (int)hipGetLastError();

@@ -21,8 +21,9 @@ from ..ops.flash_attn import flash_attn_func as _fa
 
 
 def _dropout_attn(q, k, v, causal, softmax_scale, layout, dropout_p, seed):
-    """dropout_p > 0: the chunked flash decomposition with a hashed keep mask (ops/attention_dropout.py);
-    heads are numbered globally across tensor-parallel ranks so the mask matches the unsharded model."""
+    """dropout_p > 0: dropout inside the CDNA4 flash kernels on the GPU (host path: the chunked flash
+    decomposition, ops/attention_dropout.py) with a hashed keep mask; heads are numbered globally
+    across tensor-parallel ranks so the mask matches the unsharded model."""
     from ..parallel_layers import parallel_state as ps
 
     if layout == "bshd":

@@ -67,7 +67,8 @@ class BertSelfAttention(nn.Module):
         B, S, _ = x.shape
         shp = (B, S, self.heads_local, self.head_dim)
         q, k, v = self.query(x).view(shp), self.key(x).view(shp), self.value(x).view(shp)
-        o = attention(q, k, v, causal=False, key_padding_mask=attention_mask)
+        o = attention(q, k, v, causal=False, key_padding_mask=attention_mask,
+                      dropout_p=self.dropout_p if self.training else 0.0)
         return o.reshape(B, S, self.heads_local * self.head_dim)
 
 

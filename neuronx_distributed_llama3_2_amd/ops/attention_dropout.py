@@ -1,12 +1,13 @@
 """Attention with dropout on the attention probabilities (reference: the NKI flash-attention
 kernels take `dropout_p` and a seed, src/neuronx_distributed/kernels/flash_attn.py:85-148,151-191).
 
-Llama-3 pre-training runs without attention dropout, so the hand-written CDNA4 flash kernels
-(csrc/flash_attn_*.hip) have no dropout path.  When `dropout_p > 0` is requested, this module
-runs the same flash decomposition -- query chunks, fp32 row log-sum-exp, nothing of size S x S
-kept for backward -- as batched GEMMs (hipBLASLt on the GPU) plus element-wise ops.  The keep
-mask is a counter-based hash of (seed, batch, head, query, key): nothing is stored, the backward
-regenerates exactly the forward's mask, and results do not depend on the chunking.
+On the GPU the hand-written CDNA4 flash kernels apply the dropout themselves (csrc/flash_attn_fwd.hip
+/ flash_attn_bwd.hip `DROP` variants): the keep mask is a counter-based hash of (seed, batch,
+global head, query, key) -- `dropout_keep_mask` below is its definition, shared bit-for-bit with
+the kernels' drop_row_hash / drop_keep (csrc/common.h) -- so nothing is stored and the backward
+regenerates exactly the forward's mask.  This module also holds the host path (CPU, or shapes the
+kernels do not take): the same flash decomposition -- query chunks, fp32 row log-sum-exp,
+nothing of size S x S kept for backward -- as batched GEMMs; the test oracle for the kernels.
 """
 
 from __future__ import annotations
@@ -123,4 +124,19 @@ def attention_with_dropout(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, dr
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if seed is None:
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,), generator=None).item())
+    from ._ext import use_native
+
+    if use_native(q, k, v) and q.shape[-1] in (64, 128) and q.dtype == torch.bfloat16:
+        from .flash_attn import FlashAttnFunc
+
+        qs, ks, vs = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)   # bhsd -> bshd views
+        if qs.stride(-1) != 1 or any(st % 8 for st in qs.stride()[:3]):
+            qs = qs.contiguous()
+        if ks.stride(-1) != 1 or any(st % 8 for st in ks.stride()[:3]):
+            ks = ks.contiguous()
+        if vs.stride(-1) != 1 or any(st % 8 for st in vs.stride()[:3]):
+            vs = vs.contiguous()
+        o = FlashAttnFunc.apply(qs, ks, vs, causal, scale, ks.shape[1] - qs.shape[1],
+                                (float(dropout_p), int(seed), int(head_offset)))
+        return o.transpose(1, 2)
     return DropoutAttentionFunc.apply(q, k, v, causal, scale, float(dropout_p), int(seed), int(head_offset))

@@ -43,20 +43,27 @@ def attention_reference(q, k, v, causal: bool = True, softmax_scale: Optional[fl
     return o, lse
 
 
-def _fwd(q, k, v, causal, scale, causal_offset, out=None):
+_NO_DROPOUT = (0.0, 0, 0)
+
+
+def _fwd(q, k, v, causal, scale, causal_offset, out=None, dropout=_NO_DROPOUT):
     B, Sq, Hq, D = q.shape
     o = out if out is not None else torch.empty(q.shape, dtype=q.dtype, device=q.device)
     lse = torch.empty((B, Hq, Sq), dtype=torch.float32, device=q.device)
-    ext().flash_attn_fwd(q, k, v, o, lse, float(scale), bool(causal), int(causal_offset))
+    ext().flash_attn_fwd(q, k, v, o, lse, float(scale), bool(causal), int(causal_offset), *dropout)
     return o, lse
 
 
 class FlashAttnFunc(torch.autograd.Function):
+    """dropout = (p, seed, head_offset): dropout on the probabilities inside both kernels (keep mask
+    hashed from (seed, batch, global head, query, key) -- ops/attention_dropout.dropout_keep_mask --
+    so nothing is stored and the backward regenerates it)."""
+
     @staticmethod
-    def forward(ctx, q, k, v, causal, softmax_scale, causal_offset):
-        o, lse = _fwd(q, k, v, causal, softmax_scale, causal_offset)
+    def forward(ctx, q, k, v, causal, softmax_scale, causal_offset, dropout=_NO_DROPOUT):
+        o, lse = _fwd(q, k, v, causal, softmax_scale, causal_offset, dropout=dropout)
         ctx.save_for_backward(q, k, v, o, lse)
-        ctx.causal, ctx.scale, ctx.off = causal, softmax_scale, causal_offset
+        ctx.causal, ctx.scale, ctx.off, ctx.dropout = causal, softmax_scale, causal_offset, dropout
         return o
 
     @staticmethod
@@ -66,16 +73,28 @@ class FlashAttnFunc(torch.autograd.Function):
         dq = torch.empty_like(q, memory_format=torch.contiguous_format)
         dk = torch.empty_like(k, memory_format=torch.contiguous_format)
         dv = torch.empty_like(v, memory_format=torch.contiguous_format)
-        ext().flash_attn_bwd(q, k, v, o, do, lse, dq, dk, dv, float(ctx.scale), bool(ctx.causal), int(ctx.off))
-        return dq, dk, dv, None, None, None
+        ext().flash_attn_bwd(q, k, v, o, do, lse, dq, dk, dv, float(ctx.scale), bool(ctx.causal), int(ctx.off),
+                             *ctx.dropout)
+        return dq, dk, dv, None, None, None, None
 
 
 def flash_attn_func(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True,
-                    softmax_scale: Optional[float] = None, causal_offset: Optional[int] = None) -> torch.Tensor:
-    """q: [B, Sq, Hq, D], k/v: [B, Sk, Hkv, D] (bf16, unit stride on D) -> o [B, Sq, Hq, D]."""
+                    softmax_scale: Optional[float] = None, causal_offset: Optional[int] = None,
+                    dropout_p: float = 0.0, seed: Optional[int] = None, head_offset: int = 0) -> torch.Tensor:
+    """q: [B, Sq, Hq, D], k/v: [B, Sk, Hkv, D] (bf16, unit stride on D) -> o [B, Sq, Hq, D].
+    dropout_p > 0: dropout on the attention probabilities (inverted scaling), mask from `seed`
+    with local head h drawn as global head head_offset + h (tensor-parallel ranks)."""
     D = q.shape[-1]
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
     off = (k.shape[1] - q.shape[1]) if causal_offset is None else causal_offset
+    if dropout_p:
+        from .attention_dropout import attention_with_dropout
+
+        if causal_offset is not None and causal_offset != k.shape[1] - q.shape[1]:
+            raise ValueError("dropout attention supports the bottom-right causal alignment only")
+        o = attention_with_dropout(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), dropout_p, causal=causal,
+                                   softmax_scale=scale, seed=seed, head_offset=head_offset)
+        return o.transpose(1, 2)
     if use_native(q, k, v):
         return FlashAttnFunc.apply(q, k, v, causal, scale, off)
     o, _ = attention_reference(q, k, v, causal, scale, off)
