@@ -62,6 +62,8 @@ int dgemv_launch(int, const void*, int64_t, const void*, float, const void*, int
 int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, int, hipStream_t);
 int wgrad_gemm_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int, int, int, int, hipStream_t);
 int wgrad_gemm_choose_splits(int, int, int);
+int wgrad_gemm_grouped_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int64_t, const int*, int, int,
+                              int, int, const void*, hipStream_t);
 void wgrad_gemm_set_ablate(int);
 int cu_stream_launch(const void*, void*, int64_t, int, int64_t, hipStream_t);
 int moe_combine_fwd_launch(const void*, const int64_t*, const float*, void*, int64_t, int, int, hipStream_t);
@@ -727,6 +729,25 @@ void grouped_gemm(int64_t mode, at::Tensor a, at::Tensor b, at::Tensor offs, at:
   TORCH_CHECK(offs.size(0) == E + 1, "grouped_gemm: offs must have E + 1 entries");
   TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "grouped_gemm: K and N must be multiples of 8");
   TORCH_CHECK(M < (1LL << 31) && K < (1LL << 31) && N < (1LL << 31) && E < 65536, "grouped_gemm: sizes too large");
+  static const bool wg_kernel = [] {
+    const char* e = getenv("NXD_GG_WGRAD");
+    return !(e && e[0] == '0');
+  }();
+  if (mode == 2 && wg_kernel) {
+    // expert weight gradients on the token-major wgrad kernel (csrc/wgrad_gemm.hip, grouped mode):
+    // dW[e] [K, N] += x_e^T dy_e
+    if (!accumulate) c.zero_();
+    if (M == 0) return;
+    static std::vector<at::Tensor> zeros(64);
+    const int dev = a.get_device();
+    TORCH_CHECK(dev >= 0 && dev < 64, "grouped_gemm: device index");
+    if (!zeros[dev].defined()) zeros[dev] = at::zeros({64}, a.options());
+    check_rc(nxd::wgrad_gemm_grouped_launch(a.data_ptr(), K, b.data_ptr(), N, c.data_ptr<float>(), N, K * N,
+                                            offs.data_ptr<int32_t>(), (int)E, (int)M, (int)K, (int)N,
+                                            zeros[dev].data_ptr(), cur_stream()),
+             "grouped_gemm wgrad");
+    return;
+  }
   check_rc(nxd::grouped_gemm_launch((int)mode, a.data_ptr(), b.data_ptr(), c.data_ptr(), offs.data_ptr<int32_t>(), (int)E,
                                     (int)M, (int)K, (int)N, accumulate ? 1 : 0, cur_stream()),
            "grouped_gemm");

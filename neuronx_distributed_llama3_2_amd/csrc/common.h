@@ -115,7 +115,7 @@ struct DropoutArgs {
   bool enabled() const { return thresh != 0; }
 };
 
-inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 inline int64_t ceil_div64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 }  // namespace nxd

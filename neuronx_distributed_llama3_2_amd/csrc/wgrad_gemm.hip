@@ -30,8 +30,12 @@
 //     256 contiguous bytes (MI355X_MICROARCH "Global float atomics": full rate), issued without
 //     return and left in flight when the workgroup exits; with one token split per tile each
 //     element receives exactly one add (deterministic), with S splits S adds in any order.
+//   * grouped (MoE expert weight gradients, dW[e] += x_e^T dy_e over expert-sorted rows): the grid
+//     covers (split, expert, tile); each workgroup reads its expert's row range from the device
+//     offsets (no host sync) and its ragged token tail DMAs a zero chunk instead of a foreign row.
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace nxd {
@@ -56,6 +60,11 @@ struct Params {
   int band;             // row tiles per raster band
   int ablate;           // A/B diagnostics only (wgrad_gemm_set_ablate): 1 = skip the epilogue adds,
                         // 2 = skip the MFMAs, 4 = skip the LDS-DMA refills of stages >= 3
+  // grouped mode: expert e owns rows offs[e] .. offs[e+1] of dy / x; c += e * c_es
+  const int* offs;
+  int E;
+  int64_t c_es;
+  const uint16_t* zero;   // >= 16 zero bytes: the DMA source of token rows past a group's end
 };
 
 __device__ __forceinline__ int swz(int t) { return 2 * ((t & 3) | (((t >> 3) & 1) << 2)); }
@@ -90,23 +99,39 @@ __device__ __forceinline__ void wait_vm(int newer) {   // this thread's pieces o
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+template <bool GROUPED>
 __global__ void __launch_bounds__(NT, 1) wgrad_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int tiles = p.mt * p.nt;
   const int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = id / tiles;          // splits outermost: a tile's partial sums land in different grid waves
+  const int groups = GROUPED ? p.E : 1;
+  const int split = id / (tiles * groups);   // splits outermost: a tile's partial sums land in different grid waves
+  const int ge = GROUPED ? (id / tiles) % groups : 0;
   int rt, ct;
   {
-    const int within = id - split * tiles;
+    const int within = id % tiles;
     const int kb = p.band, bnd = within / (kb * p.nt), rem = within - bnd * kb * p.nt;
     const int h = min(kb, p.mt - bnd * kb);
     rt = bnd * kb + rem % h;
     ct = rem / h;
   }
   const int m0 = rt * BM, n0 = ct * BN;
-  const int t_begin = split * p.t_per_split;
-  const int t_end = min(p.T, t_begin + p.t_per_split);
-  const int nk = (t_end - t_begin) / BK;
+  int t_begin, t_end, nk;
+  float* cbase = p.c;
+  if constexpr (GROUPED) {
+    const int g0 = p.offs[ge], g1 = p.offs[ge + 1];
+    const int per = ceil_div(ceil_div(max(g1 - g0, 0), BK), p.splits) * BK;
+    t_begin = g0 + split * per;
+    t_end = min(g1, t_begin + per);
+    if (t_begin >= t_end) return;      // empty group / split: nothing to add (workgroup-uniform)
+    nk = ceil_div(t_end - t_begin, BK);
+    cbase += ge * p.c_es;
+  } else {
+    t_begin = split * p.t_per_split;
+    t_end = min(p.T, t_begin + p.t_per_split);
+    nk = (t_end - t_begin) / BK;
+  }
+  const int rows = t_end - t_begin;   // grouped: token rows >= rows of the last stage read zeros
 
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wid >> 2, wn = wid & 3;   // 2 x 4 waves: rows 128 wm.., cols 64 wn..
@@ -122,11 +147,13 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(Params p) {
   // a stage s reads them advanced by s * BK rows (one scalar 64-bit offset per operand)
   const uint16_t* src_a[PIECES];
   const uint16_t* src_b[PIECES];
+  int tt_of[PIECES];
   {
     const int l = lane;
 #pragma unroll
     for (int i = 0; i < PIECES; ++i) {
       const int piece = wid * PIECES + i, tt = piece * 2 + (l >> 5), ch = (l & 31) ^ swz(tt);
+      tt_of[i] = tt;
       src_a[i] = p.dy + (int64_t)(t_begin + tt) * p.ld_dy + min(m0 + 8 * ch, p.M - 8);
       src_b[i] = p.x + (int64_t)(t_begin + tt) * p.ld_x + min(n0 + 8 * ch, p.N - 8);
     }
@@ -136,8 +163,13 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(Params p) {
     const int64_t oa = (int64_t)s * BK * p.ld_dy, ob = (int64_t)s * BK * p.ld_x;
 #pragma unroll
     for (int i = 0; i < PIECES; ++i) {
-      dma16(src_a[i] + oa, __builtin_amdgcn_readfirstlane(img + i * 1024));
-      dma16(src_b[i] + ob, __builtin_amdgcn_readfirstlane(img + IMG_BYTES + i * 1024));
+      const uint16_t* sa = src_a[i] + oa;
+      const uint16_t* sb = src_b[i] + ob;
+      if constexpr (GROUPED) {
+        if (s * BK + tt_of[i] >= rows) sa = sb = p.zero;   // past the group's last row: zeros
+      }
+      dma16(sa, __builtin_amdgcn_readfirstlane(img + i * 1024));
+      dma16(sb, __builtin_amdgcn_readfirstlane(img + IMG_BYTES + i * 1024));
     }
   };
 
@@ -206,7 +238,7 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(Params p) {
     for (int rr = 0; rr < 32; ++rr) {
       const int row = m0 + wm * 128 + 32 * rnd + rr;
       const float v = slab[rr * LD + lane];
-      if (row < p.M && col < p.N && !(p.ablate & 1)) unsafeAtomicAdd(p.c + (int64_t)row * p.ldc + col, v);
+      if (row < p.M && col < p.N && !(p.ablate & 1)) unsafeAtomicAdd(cbase + (int64_t)row * p.ldc + col, v);
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -268,7 +300,38 @@ int wgrad_gemm_launch(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x
   p.ablate = wg::g_ablate;
   const int64_t nwg = (int64_t)p.mt * p.nt * p.splits;
   if (nwg > INT32_MAX) return -2;
-  hipLaunchKernelGGL(wg::wgrad_kernel, dim3((unsigned)nwg), dim3(wg::NT), 0, stream, p);
+  hipLaunchKernelGGL(wg::wgrad_kernel<false>, dim3((unsigned)nwg), dim3(wg::NT), 0, stream, p);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// Grouped: c[e] [M, N] fp32 += dy[g0:g1]^T x[g0:g1] for every expert e, rows g0 = offs[e],
+// g1 = offs[e+1] read on the device; splits per group chosen for the mean group size rows / E.
+// `zero` points at >= 16 zero bytes (16-B aligned).  M % 8 == 0, N % 8 == 0.
+int wgrad_gemm_grouped_launch(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, float* c, int64_t ldc,
+                              int64_t c_es, const int* offs, int E, int rows, int M, int N, const void* zero,
+                              hipStream_t stream) {
+  if (E <= 0 || M <= 0 || N <= 0 || rows <= 0) return 0;
+  if (M % 8 || N % 8 || ld_dy % 8 || ld_x % 8) return -1;
+  wg::Params p{};
+  p.dy = static_cast<const uint16_t*>(dy);
+  p.x = static_cast<const uint16_t*>(x);
+  p.c = c;
+  p.T = rows; p.M = M; p.N = N;
+  p.ld_dy = ld_dy; p.ld_x = ld_x; p.ldc = ldc;
+  p.mt = ceil_div(M, wg::BM);
+  p.nt = ceil_div(N, wg::BN);
+  p.offs = offs;
+  p.E = E;
+  p.c_es = c_es;
+  p.zero = static_cast<const uint16_t*>(zero);
+  // splits for the mean group (all E groups' tiles share the grid)
+  const int mean = std::max(wg::BK, (rows / E) / wg::BK * wg::BK);
+  p.splits = wgrad_gemm_choose_splits(mean, (int)std::min<int64_t>((int64_t)M * E, INT32_MAX), N);
+  p.band = wg::band_rows();
+  p.ablate = wg::g_ablate;
+  const int64_t nwg = (int64_t)p.mt * p.nt * E * p.splits;
+  if (nwg > INT32_MAX) return -2;
+  hipLaunchKernelGGL(wg::wgrad_kernel<true>, dim3((unsigned)nwg), dim3(wg::NT), 0, stream, p);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
