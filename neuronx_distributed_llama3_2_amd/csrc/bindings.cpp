@@ -62,6 +62,7 @@ int dgemv_launch(int, const void*, int64_t, const void*, float, const void*, int
 int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, int, hipStream_t);
 int wgrad_gemm_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int, int, int, int, hipStream_t);
 int wgrad_gemm_choose_splits(int, int, int);
+int grouped_rowgemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, hipStream_t);
 int wgrad_gemm_grouped_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int64_t, const int*, int, int,
                               int, int, const void*, hipStream_t);
 void wgrad_gemm_set_ablate(int);
@@ -747,6 +748,19 @@ void grouped_gemm(int64_t mode, at::Tensor a, at::Tensor b, at::Tensor offs, at:
                                             zeros[dev].data_ptr(), cur_stream()),
              "grouped_gemm wgrad");
     return;
+  }
+  static const bool row_kernel = [] {
+    const char* e = getenv("NXD_GG_ROW");
+    return !(e && e[0] == '0');
+  }();
+  if ((mode == 0 || mode == 1) && row_kernel) {
+    // 256 x 256 tiles (csrc/grouped_rowgemm.hip); -1 = shape it does not take (reduction % 32)
+    const int rc = nxd::grouped_rowgemm_launch((int)mode, a.data_ptr(), b.data_ptr(), c.data_ptr(),
+                                               offs.data_ptr<int32_t>(), (int)E, (int)M, (int)K, (int)N, cur_stream());
+    if (rc != -1) {
+      check_rc(rc, "grouped_gemm (256-tile)");
+      return;
+    }
   }
   check_rc(nxd::grouped_gemm_launch((int)mode, a.data_ptr(), b.data_ptr(), c.data_ptr(), offs.data_ptr<int32_t>(), (int)E,
                                     (int)M, (int)K, (int)N, accumulate ? 1 : 0, cur_stream()),

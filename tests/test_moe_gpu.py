@@ -42,6 +42,7 @@ def _ref_fwd(x, w, offs):
     ([64, 200, 0, 3], 264, 392),                       # k / n tails (multiples of 8 only)
     ([0, 0, 0, 0], 128, 128),                          # no rows at all
     ([4096], 512, 640),                                # one big group
+    ([1000, 0, 37, 700, 3, 513], 512, 1056),           # 256-tile kernels: ragged rows, partial column tiles
 ])
 def test_grouped_gemm_fwd_dgrad_wgrad(counts, K, N):
     E = len(counts)

@@ -1,0 +1,8 @@
+#!/bin/bash
+# 256-tile grouped fwd / dgrad: numerics, GEMM TF/s, Mixtral 4L.
+set -o pipefail
+O=gpurun_out/r3moe2; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_moe_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || exit $?
+timeout -k 10 300 python -u tools/bench_grouped_gemm.py > $O/grouped_gemm.jsonl 2>&1 || exit $?
+timeout -k 10 600 python -u tools/bench_mixtral_train.py --layers 4 --seq 4096 --mbs 2 --accum 4 --steps 3 > $O/mixtral_train.jsonl 2> $O/mixtral_train.err || exit $?
