@@ -64,7 +64,7 @@ int wgrad_gemm_launch(const void*, int64_t, const void*, int64_t, float*, int64_
 int wgrad_gemm_choose_splits(int, int, int);
 int grouped_rowgemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, hipStream_t);
 int wgrad_gemm_grouped_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int64_t, const int*, int, int,
-                              int, int, const void*, hipStream_t);
+                              int, int, hipStream_t);
 void wgrad_gemm_set_ablate(int);
 int cu_stream_launch(const void*, void*, int64_t, int, int64_t, hipStream_t);
 int moe_combine_fwd_launch(const void*, const int64_t*, const float*, void*, int64_t, int, int, hipStream_t);
@@ -739,13 +739,8 @@ void grouped_gemm(int64_t mode, at::Tensor a, at::Tensor b, at::Tensor offs, at:
     // dW[e] [K, N] += x_e^T dy_e
     if (!accumulate) c.zero_();
     if (M == 0) return;
-    static std::vector<at::Tensor> zeros(64);
-    const int dev = a.get_device();
-    TORCH_CHECK(dev >= 0 && dev < 64, "grouped_gemm: device index");
-    if (!zeros[dev].defined()) zeros[dev] = at::zeros({64}, a.options());
     check_rc(nxd::wgrad_gemm_grouped_launch(a.data_ptr(), K, b.data_ptr(), N, c.data_ptr<float>(), N, K * N,
-                                            offs.data_ptr<int32_t>(), (int)E, (int)M, (int)K, (int)N,
-                                            zeros[dev].data_ptr(), cur_stream()),
+                                            offs.data_ptr<int32_t>(), (int)E, (int)M, (int)K, (int)N, cur_stream()),
              "grouped_gemm wgrad");
     return;
   }

@@ -30,9 +30,10 @@
 namespace nxd {
 namespace grg {
 
-constexpr int BM = 256, BN = 256, BK = 32, NT = 512;
+constexpr int BM = 256, BN = 256, BK = 32, STAGES = 4, NT = 512;
 constexpr int IMG_BYTES = 256 * BK * 2;            // 16 KiB: one operand stage
 constexpr int STAGE_BYTES = 2 * IMG_BYTES;
+constexpr int LDS_BYTES = STAGES * STAGE_BYTES;    // 128 KiB
 constexpr int PIECES = IMG_BYTES / 1024 / (NT / 64);   // 2 per wave per operand
 constexpr int DMA_PER_STAGE = 2 * PIECES;
 enum Mode { FWD = 0, DGRAD = 1 };
@@ -84,17 +85,17 @@ __device__ __forceinline__ bf16x8_t frag_tr(const char* img, int c0) {
   return __builtin_bit_cast(bf16x8_t, a8);
 }
 
-// this thread's pieces of the oldest outstanding stage landed, `newer` younger stages left in flight
+// this thread's pieces of the oldest outstanding stage landed (`newer` younger stages left in flight)
 __device__ __forceinline__ void wait_vm(int newer) {
-  if (newer >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DMA_PER_STAGE) : "memory");
-  else if (newer == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_STAGE) : "memory");
+  if (newer >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_STAGE) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// STAGES: LDS ring depth (4 = 128 KiB, 5 = 160 KiB: one more stage of DMA latency cover)
-template <int MODE, int STAGES>
+// Measured and not kept (profiles/r3_grouped_rowgemm_variants.jsonl): a 5-stage ring (160 KiB) and
+// s_setprio around the MFMA clusters or for the younger wave half -- all within +-2 %.
+template <int MODE>
 __global__ void __launch_bounds__(NT, 1) rowgemm_kernel(Params p) {
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   int rt, ct;
   {
@@ -224,19 +225,11 @@ __global__ void __launch_bounds__(NT, 1) rowgemm_kernel(Params p) {
   }
 }
 
-static int ring_stages() {
-  static const int s = [] {
-    const char* e = getenv("NXD_GRG_STAGES");
-    return e && atoi(e) == 5 ? 5 : 4;
-  }();
-  return s;
-}
-
 static int band_rows() {
   static const int b = [] {
-    const char* e = getenv("NXD_GRG_BAND");
-    const int v = e ? atoi(e) : 4;
-    return v > 0 ? v : 4;
+    const char* e = getenv("NXD_GRG_BAND");   // 8: +2..7 % over 4 on most Mixtral shapes (r3_grouped_rowgemm_variants)
+    const int v = e ? atoi(e) : 8;
+    return v > 0 ? v : 8;
   }();
   return b;
 }
@@ -273,13 +266,10 @@ int grouped_rowgemm_launch(int mode, const void* a, const void* w, void* c, cons
   p.band = grg::band_rows();
   const int64_t nwg = (int64_t)p.rt * p.nt;
   if (nwg > INT32_MAX) return -2;
-#define NXD_GRG_LAUNCH(M, S) hipLaunchKernelGGL((grg::rowgemm_kernel<M, S>), dim3((unsigned)nwg), dim3(grg::NT), 0, stream, p)
-  if (grg::ring_stages() == 5) {
-    if (mode == grg::FWD) NXD_GRG_LAUNCH(grg::FWD, 5); else NXD_GRG_LAUNCH(grg::DGRAD, 5);
-  } else {
-    if (mode == grg::FWD) NXD_GRG_LAUNCH(grg::FWD, 4); else NXD_GRG_LAUNCH(grg::DGRAD, 4);
-  }
-#undef NXD_GRG_LAUNCH
+if (mode == grg::FWD)
+    hipLaunchKernelGGL(grg::rowgemm_kernel<grg::FWD>, dim3((unsigned)nwg), dim3(grg::NT), 0, stream, p);
+  else
+    hipLaunchKernelGGL(grg::rowgemm_kernel<grg::DGRAD>, dim3((unsigned)nwg), dim3(grg::NT), 0, stream, p);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

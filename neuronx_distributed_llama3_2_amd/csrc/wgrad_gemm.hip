@@ -64,8 +64,10 @@ struct Params {
   const int* offs;
   int E;
   int64_t c_es;
-  const uint16_t* zero;   // >= 16 zero bytes: the DMA source of token rows past a group's end
 };
+
+__device__ __attribute__((aligned(16))) uint32_t g_zero16[4];   // zero-initialised device global: the DMA
+                                                                  // source of token rows past a group's end
 
 __device__ __forceinline__ int swz(int t) { return 2 * ((t & 3) | (((t >> 3) & 1) << 2)); }
 __device__ __forceinline__ int img_off(int t, int ch) { return t * 512 + 16 * (ch ^ swz(t)); }
@@ -99,6 +101,8 @@ __device__ __forceinline__ void wait_vm(int newer) {   // this thread's pieces o
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// s_setprio around the MFMA clusters or for the younger wave half measured within +-2 % (not kept,
+// profiles/r3_wgrad_kernel_prio_rejected.jsonl)
 template <bool GROUPED>
 __global__ void __launch_bounds__(NT, 1) wgrad_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
@@ -166,7 +170,7 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(Params p) {
       const uint16_t* sa = src_a[i] + oa;
       const uint16_t* sb = src_b[i] + ob;
       if constexpr (GROUPED) {
-        if (s * BK + tt_of[i] >= rows) sa = sb = p.zero;   // past the group's last row: zeros
+        if (s * BK + tt_of[i] >= rows) sa = sb = reinterpret_cast<const uint16_t*>(g_zero16);   // past the group's end
       }
       dma16(sa, __builtin_amdgcn_readfirstlane(img + i * 1024));
       dma16(sb, __builtin_amdgcn_readfirstlane(img + IMG_BYTES + i * 1024));
@@ -255,6 +259,11 @@ static int band_rows() {
 
 static int g_ablate = 0;
 
+template <bool G>
+void launch(const Params& p, int64_t nwg, hipStream_t stream) {
+  hipLaunchKernelGGL((wgrad_kernel<G>), dim3((unsigned)nwg), dim3(NT), 0, stream, p);
+}
+
 }  // namespace wg
 
 void wgrad_gemm_set_ablate(int v) { wg::g_ablate = v; }
@@ -300,16 +309,15 @@ int wgrad_gemm_launch(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x
   p.ablate = wg::g_ablate;
   const int64_t nwg = (int64_t)p.mt * p.nt * p.splits;
   if (nwg > INT32_MAX) return -2;
-  hipLaunchKernelGGL(wg::wgrad_kernel<false>, dim3((unsigned)nwg), dim3(wg::NT), 0, stream, p);
+  wg::launch<false>(p, nwg, stream);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 // Grouped: c[e] [M, N] fp32 += dy[g0:g1]^T x[g0:g1] for every expert e, rows g0 = offs[e],
 // g1 = offs[e+1] read on the device; splits per group chosen for the mean group size rows / E.
-// `zero` points at >= 16 zero bytes (16-B aligned).  M % 8 == 0, N % 8 == 0.
+// M % 8 == 0, N % 8 == 0.
 int wgrad_gemm_grouped_launch(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, float* c, int64_t ldc,
-                              int64_t c_es, const int* offs, int E, int rows, int M, int N, const void* zero,
-                              hipStream_t stream) {
+                              int64_t c_es, const int* offs, int E, int rows, int M, int N, hipStream_t stream) {
   if (E <= 0 || M <= 0 || N <= 0 || rows <= 0) return 0;
   if (M % 8 || N % 8 || ld_dy % 8 || ld_x % 8) return -1;
   wg::Params p{};
@@ -323,7 +331,6 @@ int wgrad_gemm_grouped_launch(const void* dy, int64_t ld_dy, const void* x, int6
   p.offs = offs;
   p.E = E;
   p.c_es = c_es;
-  p.zero = static_cast<const uint16_t*>(zero);
   // splits for the mean group (all E groups' tiles share the grid)
   const int mean = std::max(wg::BK, (rows / E) / wg::BK * wg::BK);
   p.splits = wgrad_gemm_choose_splits(mean, (int)std::min<int64_t>((int64_t)M * E, INT32_MAX), N);
@@ -331,7 +338,7 @@ int wgrad_gemm_grouped_launch(const void* dy, int64_t ld_dy, const void* x, int6
   p.ablate = wg::g_ablate;
   const int64_t nwg = (int64_t)p.mt * p.nt * E * p.splits;
   if (nwg > INT32_MAX) return -2;
-  hipLaunchKernelGGL(wg::wgrad_kernel<true>, dim3((unsigned)nwg), dim3(wg::NT), 0, stream, p);
+  wg::launch<true>(p, nwg, stream);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -80,17 +80,16 @@ def _use_wgrad_t(go2: torch.Tensor, x2: torch.Tensor = None, K: int = None) -> b
 # the hardware transpose read and splits the token range over workgroups.  Measured against this
 # module's hipBLASLt path (profiles/r3_wgrad_kernel_vs_hipblaslt.jsonl): faster on the skinny
 # tensor-parallel shards -- TP=8 qkv 984 vs 743 TF/s, o 880 vs 717 (M*N/(M+N) < 1100) -- and
-# 5-13 % slower than the bare TN GEMM on the large TP=1 shapes.  But the TN GEMM needs both operands
-# transposed unless their producers wrote token-major copies; counting the two transposes it loses
-# at TP=1 qkv (0.391 + 0.067 vs 0.441 ms) and o (0.251 + 0.054 vs 0.260 ms) and ties lm_head.  So
-# `auto` takes the kernel for skinny shards, and for any shape where neither operand has a
-# producer-written copy (qkv, o_proj, lm_head; gate_up / down keep the SwiGLU-written copies).
+# 5-13 % slower than the bare TN GEMM on the large TP=1 shapes.  Counting the TN path's two operand
+# transposes the isolated kernel should also win TP=1 qkv / o_proj, but inside the TP=1 step that
+# routing measured +4.6 ms per 2 micro-batches (GEMM + wgrad kernel + transposes 531.9 vs 527.3 ms,
+# profiles/r3_step_breakdown_wgrad_all_nocopy_rejected.txt), so `auto` keeps the skinny rule.
 # NXD_WGRAD_KERNEL = auto | 1 (whenever the shapes allow) | 0.
 _WG_KERNEL = os.environ.get("NXD_WGRAD_KERNEL", "auto")
 _WG_SKINNY = 1100.0
 
 
-def _use_wgrad_kernel(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor, have_copy: bool = False) -> bool:
+def _use_wgrad_kernel(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor) -> bool:
     if _WG_KERNEL == "0" or x2 is None or not _native(go2, x2) or mg.dtype != torch.float32:
         return False
     T, M = go2.shape
@@ -99,7 +98,7 @@ def _use_wgrad_kernel(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor, hav
         return False
     if go2.stride(0) % 8 or x2.stride(0) % 8 or go2.data_ptr() % 16 or x2.data_ptr() % 16:
         return False
-    return _WG_KERNEL == "1" or M * N / (M + N) < _WG_SKINNY or not have_copy
+    return _WG_KERNEL == "1" or M * N / (M + N) < _WG_SKINNY
 
 
 def _wgrad_scratch(n: int, dtype, device, tag: str = "") -> torch.Tensor:
@@ -122,7 +121,7 @@ def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2, go_t: torch.Tenso
     into a reused scratch, then an fp32 add (the per-micro-batch weight gradient is rounded to
     bf16 before the fp32 accumulation — the precision of the reference's XLA matmul + fp32
     grad accumulation; hipBLASLt's bf16-output solutions run faster than its fp32-output ones)."""
-    if _use_wgrad_kernel(mg, go2, x2, have_copy=go_t is not None or x_t is not None):
+    if _use_wgrad_kernel(mg, go2, x2):
         ext().wgrad_gemm(mg, go2, x2, 0)
         return
     if x_t is not None and not (x_t.dim() == 2 and x_t.is_contiguous() and x_t.shape[1] == go2.shape[0]):

@@ -31,6 +31,7 @@ def timed(fn, reps):
 
 def main():
     only = sys.argv[1:]
+    G._WG_KERNEL = "0"   # the comparison arm is the hipBLASLt path (the framework default routes skinny shards to the kernel)
     for name, tp, T, M, N in SHAPES:
         if only and f"{name}{tp}" not in only:
             continue
