@@ -46,23 +46,12 @@ def main():
             r["dgrad_grouped_tf"] = fl / timed(lambda: C.grouped_gemm(1, dy, w, offs, dx, False)) / 1e9
             r["wgrad_grouped_tf"] = fl / timed(lambda: C.grouped_gemm(2, x, dy, offs, dw, True)) / 1e9
 
-            def loop_fwd():
-                s = 0
-                for e, n in enumerate(counts):
-                    torch.matmul(x[s:s + n], w[e], out=y[s:s + n])
-                    s += n
+            from neuronx_distributed_llama3_2_amd.ops.grouped_gemm import _loop_dgrad, _loop_fwd, _loop_wgrad
 
-            def loop_dgrad():
-                s = 0
-                for e, n in enumerate(counts):
-                    torch.matmul(dy[s:s + n], w[e].t(), out=dx[s:s + n])
-                    s += n
-
-            def loop_wgrad():
-                s = 0
-                for e, n in enumerate(counts):
-                    dw[e].add_(torch.matmul(x[s:s + n].t(), dy[s:s + n]).float())
-                    s += n
+            bounds = offs.tolist()   # the framework's loop backend (NXD_MOE_GEMM=loop): fp32-output addmm wgrad
+            loop_fwd = lambda: _loop_fwd(x, w, bounds, y)  # noqa: E731
+            loop_dgrad = lambda: _loop_dgrad(dy, w, bounds, dx)  # noqa: E731
+            loop_wgrad = lambda: _loop_wgrad(x, dy, bounds, dw, True)  # noqa: E731
 
             r["fwd_loop_tf"] = fl / timed(loop_fwd) / 1e9
             r["dgrad_loop_tf"] = fl / timed(loop_dgrad) / 1e9
