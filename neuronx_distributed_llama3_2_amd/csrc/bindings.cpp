@@ -58,10 +58,12 @@ void decode_attn_set_v2(int);
 void decode_attn_set_prefetch(const void*, int64_t, const void*, int64_t, int);
 int dgemv_launch(int, const void*, int64_t, const void*, float, const void*, int64_t, void*, int64_t, int, int, int, int,
                  int, int, const float*, const float*, const int64_t*, int, void*, void*, int64_t, int64_t, int64_t,
-                 const int*, int, int, hipStream_t);
+                 const int*, int, int, const float*, float*, hipStream_t);
 int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, int, hipStream_t);
 int wgrad_gemm_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int, int, int, int, hipStream_t);
 int wgrad_gemm_choose_splits(int, int, int);
+int decode_attn_oproj_launch(const void*, const int64_t*, const void*, const void*, const int64_t*, const int*, const int*,
+                             const void*, int64_t, int, float*, int, int, int, int, int, int, float, hipStream_t);
 int grouped_rowgemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, hipStream_t);
 int wgrad_gemm_grouped_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int64_t, const int*, int, int,
                               int, int, hipStream_t);
@@ -468,6 +470,44 @@ void decode_attn_prefetch(c10::optional<at::Tensor> a, int64_t a_bytes, c10::opt
   nxd::decode_attn_set_prefetch(ra.first, ra.second, rb.first, rb.second, (int)wgs);
 }
 
+// Fused decode attention + o_proj (csrc/decode_attn.hip FUSE): oacc [B*T, Hout] fp32 (zero on entry)
+// += o_proj(attention).  Returns false (nothing launched) for shapes the fused kernel does not cover.
+bool decode_attn_oproj(at::Tensor q, at::Tensor kc, at::Tensor vc, c10::optional<at::Tensor> cache_idx, at::Tensor seq_len,
+                       at::Tensor wo, at::Tensor oacc, double scale) {
+  int64_t qs[3];
+  bshd_strides(q, "q", qs);
+  check_bf16(kc, "k_cache");
+  check_bf16(vc, "v_cache");
+  check_bf16(wo, "wo");
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.sizes() == kc.sizes() && vc.is_contiguous(),
+              "caches must be contiguous [B, Hkv, Lmax, D]");
+  const int B = q.size(0), T = q.size(1), Hq = q.size(2), D = q.size(3);
+  const int Hkv = kc.size(1), Lmax = kc.size(2);
+  TORCH_CHECK(kc.size(3) == D, "head dim mismatch");
+  TORCH_CHECK(wo.dim() == 2 && wo.stride(1) == 1 && wo.size(1) == (int64_t)Hq * D, "wo must be [Hout, Hq * D]");
+  check_aligned16(wo, "wo");
+  const int64_t Hout = wo.size(0);
+  TORCH_CHECK(oacc.scalar_type() == at::kFloat && oacc.is_cuda() && oacc.is_contiguous() && oacc.dim() == 2 &&
+                  oacc.size(0) >= (int64_t)B * T && oacc.size(1) == Hout,
+              "oacc must be fp32 contiguous [>= B*T, Hout]");
+  TORCH_CHECK(seq_len.scalar_type() == at::kInt && seq_len.numel() == B && seq_len.is_contiguous(), "seq_len must be int32 [B]");
+  const int* ci = nullptr;
+  if (cache_idx.has_value()) {
+    TORCH_CHECK(cache_idx->scalar_type() == at::kInt && cache_idx->numel() == B, "cache_idx must be int32 [B]");
+    ci = cache_idx->data_ptr<int>();
+  } else {
+    TORCH_CHECK(kc.size(0) >= B, "cache batch too small");
+  }
+  if (Hkv <= 0 || Hq % Hkv || Hout > INT32_MAX) return false;
+  const int64_t cs[3] = {kc.stride(0), kc.stride(1), kc.stride(2)};
+  const int rc = nxd::decode_attn_oproj_launch(q.data_ptr(), qs, kc.data_ptr(), vc.data_ptr(), cs, ci, seq_len.data_ptr<int>(),
+                                               wo.data_ptr(), wo.stride(0), (int)Hout, oacc.data_ptr<float>(), B, T, Hq, Hkv, D,
+                                               Lmax, (float)scale, cur_stream());
+  if (rc == -1) return false;
+  check_rc(rc, "decode_attn_oproj");
+  return true;
+}
+
 void decode_attn(at::Tensor q, at::Tensor kc, at::Tensor vc, c10::optional<at::Tensor> cache_idx, at::Tensor seq_len,
                  at::Tensor out, double scale, int64_t nsplit) {
   int64_t qs[3], os[3];
@@ -813,7 +853,7 @@ void moe_combine_bwd(at::Tensor dout, at::Tensor ys, at::Tensor inv, at::Tensor 
 void dgemv(int64_t epi, at::Tensor x, c10::optional<at::Tensor> norm_w, double eps, at::Tensor w, at::Tensor y,
            int64_t nq, int64_t nkv, int64_t D, c10::optional<at::Tensor> cos_t, c10::optional<at::Tensor> sin_t,
            c10::optional<at::Tensor> pos, int64_t T, c10::optional<at::Tensor> kc, c10::optional<at::Tensor> vc,
-           c10::optional<at::Tensor> cache_idx) {
+           c10::optional<at::Tensor> cache_idx, c10::optional<at::Tensor> xadd, c10::optional<at::Tensor> yadd) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_bf16(y, "y");
@@ -873,9 +913,27 @@ void dgemv(int64_t epi, at::Tensor x, c10::optional<at::Tensor> norm_w, double e
   } else {
     TORCH_CHECK(epi >= 0 && epi <= 2, "dgemv: epi must be 0..3");
   }
+  // fp32 pending-residual side inputs (fused attention + o_proj): xadd [M, K] for the NORM prologue,
+  // yadd [M, N] for the RESID epilogue (zeroed by it)
+  const float* xa = nullptr;
+  float* ya = nullptr;
+  if (xadd.has_value()) {
+    TORCH_CHECK(nw != nullptr, "dgemv: xadd needs the fused RMSNorm prologue");
+    TORCH_CHECK(xadd->scalar_type() == at::kFloat && xadd->is_contiguous() && xadd->dim() == 2 && xadd->size(0) >= M &&
+                    xadd->size(1) == K && xadd->is_cuda(),
+                "dgemv: xadd fp32 contiguous [>=M, K]");
+    xa = xadd->data_ptr<float>();
+  }
+  if (yadd.has_value()) {
+    TORCH_CHECK(epi == 1, "dgemv: yadd is the RESID epilogue's side input");
+    TORCH_CHECK(yadd->scalar_type() == at::kFloat && yadd->is_contiguous() && yadd->dim() == 2 && yadd->size(0) >= M &&
+                    yadd->size(1) == N && yadd->is_cuda(),
+                "dgemv: yadd fp32 contiguous [>=M, N]");
+    ya = yadd->data_ptr<float>();
+  }
   check_rc(nxd::dgemv_launch((int)epi, x.data_ptr(), x.stride(0), nw, (float)eps, w.data_ptr(), w.stride(0), y.data_ptr(),
                              y.stride(0), (int)M, (int)N, (int)K, (int)nq, (int)nkv, (int)D, cp, sp, pp, (int)T, kp, vp,
-                             c_sb, c_sh, c_sl, ci, Lmax, max_pos, cur_stream()),
+                             c_sb, c_sh, c_sl, ci, Lmax, max_pos, xa, ya, cur_stream()),
            "dgemv");
 }
 
@@ -907,7 +965,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("wgrad_gemm_splits", [](int64_t T, int64_t M, int64_t N) { return nxd::wgrad_gemm_choose_splits((int)T, (int)M, (int)N); });
   m.def("moe_combine_fwd", &moe_combine_fwd);
   m.def("moe_combine_bwd", &moe_combine_bwd);
-  m.def("dgemv", &dgemv);
+  m.def("dgemv", &dgemv, py::arg("epi"), py::arg("x"), py::arg("norm_w"), py::arg("eps"), py::arg("w"), py::arg("y"),
+        py::arg("nq"), py::arg("nkv"), py::arg("D"), py::arg("cos_t"), py::arg("sin_t"), py::arg("pos"), py::arg("T"),
+        py::arg("kc"), py::arg("vc"), py::arg("cache_idx"), py::arg("xadd") = py::none(), py::arg("yadd") = py::none());
   // decode A/B knobs: 0 = GLU row pairs per wave, 1 = GEMV k-slices (0 auto), 2 = MFMA decode attention on/off
   m.def("decode_set_knob", [](int which, int value) {
     if (which == 2) nxd::decode_attn_set_v2(value);
@@ -939,6 +999,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("decode_attn", &decode_attn);
+  m.def("decode_attn_oproj", &decode_attn_oproj);
   m.def("decode_attn_prefetch", &decode_attn_prefetch);
   m.def("kv_cache_write", &kv_cache_write);
   m.def("argmax_rows", &argmax_rows);

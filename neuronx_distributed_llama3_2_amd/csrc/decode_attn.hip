@@ -13,7 +13,18 @@
 // keys) the workgroup writes the final bf16 output; otherwise it writes the (m, l, o) partials that
 // inference.hip's merge kernel combines.  Compared with the 128-key-chunk kernel there (four
 // workgroup barriers per chunk and a merge launch at every length) this is one barrier per call.
+//
+// FUSE (attention + o_proj, one launch instead of two): the grid is (batch, kv head, R row chunks
+// of the o_proj output); every workgroup of a kv head recomputes that head group's attention (a
+// few hundred L2-resident keys at decode lengths) and multiplies it by its Wo block [H/R rows x
+// G*D columns], prefetched into registers before the attention starts, then adds the partial
+// rows into an fp32 accumulator with float atomics (G*D columns of the o_proj reduction per
+// workgroup).  No cross-workgroup wait: the next launch (the GLU projection's RMSNorm prologue and
+// the down projection's residual epilogue, decode_fused.hip xadd / yadd) folds the accumulator into
+// the residual stream with the rounding of the unfused o_proj epilogue and zeroes it.
 #include "common.h"
+
+#include <cstdlib>
 
 namespace nxd {
 namespace dattn {
@@ -42,6 +53,11 @@ struct Params {
   const u32x4_t* pf[2];
   int64_t pf_n16[2];   // 16-byte chunks per range
   int attn_wgs;
+  // FUSE: o_proj weight [Hout, Hq * D] (row stride ldwo), fp32 accumulator [B * T, Hout]
+  const uint16_t* wo;
+  int64_t ldwo;
+  float* oacc;
+  int Hout, R, NP;     // output rows, row chunks per kv head, Wo register passes (<= 4)
 };
 
 // Prefetch workgroup body: 4 independent 16-B loads in flight per lane, folded into one value that
@@ -66,7 +82,7 @@ __device__ __forceinline__ void prefetch_body(const Params& p, int wg, int nwg) 
 typedef __attribute__((address_space(3))) short4_t lds_s4_t;
 typedef short short8_t __attribute__((ext_vector_type(8)));
 
-template <int D, int NWV>
+template <int D, int NWV, bool FUSE>
 __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
   constexpr int NS = D / 32;      // k-steps of the score MFMA
   constexpr int NDT = D / 16;     // 16-wide d tiles of the output
@@ -79,14 +95,32 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
   float* red_m = red_o + NWV * 16 * D;                                          // [NWV][16]
   float* red_l = red_m + NWV * 16;
 
-  if ((int)blockIdx.x >= p.attn_wgs) {
+  if (!FUSE && (int)blockIdx.x >= p.attn_wgs) {
     prefetch_body(p, blockIdx.x - p.attn_wgs, gridDim.x - p.attn_wgs);
     return;
   }
-  const int split = blockIdx.x % p.nsplit;
-  const int bh = blockIdx.x / p.nsplit;
+  const int split = FUSE ? 0 : (int)blockIdx.x % p.nsplit;
+  const int bh = FUSE ? (int)blockIdx.x / p.R : (int)blockIdx.x / p.nsplit;
   const int b = bh / p.Hkv, hkv = bh % p.Hkv;
   const int G = p.Hq / p.Hkv, M = G * p.T;
+  // FUSE: this workgroup's Wo block (rows rc * NR .., columns of head group hkv) into registers,
+  // issued before the attention so its HBM latency hides behind it.  Thread (row r0 + pass * RPP,
+  // 32-column segment seg).
+  const int tpr = FUSE ? (G * D) / 32 : 1;
+  const int seg = tid % tpr, r0 = tid / tpr, rpp = (64 * NWV) / tpr;
+  const int nr = FUSE ? p.Hout / p.R : 0;
+  const int row0 = FUSE ? ((int)blockIdx.x % p.R) * nr + r0 : 0;
+  u32x4_t wreg[4][4];
+  if constexpr (FUSE) {
+    const uint16_t* wb = p.wo + (int64_t)row0 * p.ldwo + (int64_t)hkv * G * D + 32 * seg;
+#pragma unroll
+    for (int np = 0; np < 4; ++np) {
+      if (np < p.NP) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wreg[np][j] = *reinterpret_cast<const u32x4_t*>(wb + (int64_t)np * rpp * p.ldwo + 8 * j);
+      }
+    }
+  }
   const int cb = p.cache_idx ? p.cache_idx[b] : b;
   const int slen = p.seq_len[b];
   const uint16_t* kbase = p.kc + (int64_t)cb * p.c_sb + (int64_t)hkv * p.c_sh;
@@ -240,7 +274,9 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
       L += wt * red_l[w * 16 + m];
       acc += wt * red_o[(w * 16 + m) * D + d];
     }
-    if (p.nsplit == 1) {
+    if (FUSE) {   // bf16-rounded as the unfused path's attention output, then o_proj below
+      reinterpret_cast<float*>(smem)[m * D + d] = bf2f(f2bf(L > 0.f ? acc / L : 0.f));
+    } else if (p.nsplit == 1) {
       const int tt = m / G, gg = m % G;
       p.out[(int64_t)b * p.o_sb + (int64_t)tt * p.o_st + (int64_t)(hkv * G + gg) * p.o_sh + d] =
           f2bf(L > 0.f ? acc / L : 0.f);
@@ -249,6 +285,31 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
       if (d == 0) {
         p.pm[pbase + m] = gm == -INFINITY ? -INFINITY : gm * 0.69314718056f;   // log2 -> natural-log domain
         p.pl[pbase + m] = L;
+      }
+    }
+  }
+  if constexpr (FUSE) {
+    // ---- o_proj partial of this head group: out[t][row] += sum_c Wo[row][hkv*G*D + c] o[t][c]
+    __syncthreads();
+    const float* of = reinterpret_cast<const float*>(smem);   // [M][D] attention output (m = t * G + g)
+    const int c0 = 32 * seg, gg = c0 / D, d0 = c0 % D;
+#pragma unroll
+    for (int np = 0; np < 4; ++np) {
+      if (np >= p.NP) break;
+      float w[32];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) unpack8(wreg[np][j], w + 8 * j);
+      const int row = row0 + np * rpp;
+      for (int tt = 0; tt < p.T; ++tt) {
+        const float* orow = of + (tt * G + gg) * D + d0;
+        float dot = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; j += 4) {
+          const f32x4_t o4 = *reinterpret_cast<const f32x4_t*>(orow + j);
+          dot += w[j] * o4[0] + w[j + 1] * o4[1] + w[j + 2] * o4[2] + w[j + 3] * o4[3];
+        }
+        for (int off = tpr / 2; off > 0; off >>= 1) dot += __shfl_xor(dot, off, 64);
+        if (seg == 0) unsafeAtomicAdd(p.oacc + (int64_t)(b * p.T + tt) * p.Hout + row, dot);
       }
     }
   }
@@ -304,11 +365,57 @@ int decode_attn2_launch(const void* q, const int64_t* qs, const void* kc, const 
   dattn::g_pf_bytes[0] = dattn::g_pf_bytes[1] = 0;
   const dim3 grid(p.attn_wgs + pf_wgs), block(64 * nwv);
   if (D == 64) {
-    (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<64, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((dattn::attn_kernel<64, 8>), grid, block, lds, stream, p);
+    (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<64, 8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((dattn::attn_kernel<64, 8, false>), grid, block, lds, stream, p);
   } else {
-    (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<128, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((dattn::attn_kernel<128, 4>), grid, block, lds, stream, p);
+    (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<128, 4, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((dattn::attn_kernel<128, 4, false>), grid, block, lds, stream, p);
+  }
+  return (int)hipGetLastError();
+}
+
+// Fused decode attention + o_proj (see FUSE above): oacc [B*T, Hout] fp32 must be zero on entry
+// (the down projection's RESID epilogue re-zeroes it).  Returns -1 when the shape is not covered:
+// one key split (Lmax <= 1024), M = G*T <= 16, D in {64, 128}, Wo blocks of <= 4 register passes.
+int decode_attn_oproj_launch(const void* q, const int64_t* qs, const void* kc, const void* vc, const int64_t* cs,
+                             const int* cache_idx, const int* seq_len, const void* wo, int64_t ldwo, int Hout, float* oacc,
+                             int B, int T, int Hq, int Hkv, int D, int Lmax, float scale, hipStream_t stream) {
+  if (Hkv <= 0 || Hq % Hkv) return -1;
+  const int G = Hq / Hkv, M = G * T;
+  if (M > 16 || (D != 64 && D != 128) || Lmax > dattn::KPS || (G * D) % 32 || ldwo % 8) return -1;
+  const int nwv = D == 64 ? 8 : 4;
+  const int nt = 64 * nwv, tpr = (G * D) / 32;
+  if (tpr > 64 || 64 % tpr || nt % tpr) return -1;
+  const int rpp = nt / tpr;
+  // row chunks per kv head: fill >= target workgroups (NXD_DECODE_OPROJ_WGS, default 256), at most 4
+  // register passes per thread
+  static const int target = [] {
+    const char* e = getenv("NXD_DECODE_OPROJ_WGS");
+    const int v = e ? atoi(e) : 256;
+    return v > 0 ? v : 256;
+  }();
+  int R = 1;
+  while ((int64_t)B * Hkv * R < target && Hout % (2 * R) == 0 && (Hout / (2 * R)) % rpp == 0) R *= 2;
+  while (Hout % R == 0 && (Hout / R) % rpp == 0 && Hout / R / rpp > 4 && Hout % (2 * R) == 0 && (Hout / (2 * R)) % rpp == 0)
+    R *= 2;
+  if (Hout % R || (Hout / R) % rpp || Hout / R / rpp > 4 || Hout / R / rpp < 1) return -1;
+  dattn::Params p{};
+  p.q = (const uint16_t*)q; p.q_sb = qs[0]; p.q_st = qs[1]; p.q_sh = qs[2];
+  p.kc = (const uint16_t*)kc; p.vc = (const uint16_t*)vc;
+  p.c_sb = cs[0]; p.c_sh = cs[1]; p.c_sl = cs[2];
+  p.cache_idx = cache_idx; p.seq_len = seq_len;
+  p.B = B; p.T = T; p.Hq = Hq; p.Hkv = Hkv; p.nsplit = 1;
+  p.scale_log2 = scale * 1.4426950408889634f;
+  p.wo = (const uint16_t*)wo; p.ldwo = ldwo; p.oacc = oacc; p.Hout = Hout; p.R = R; p.NP = Hout / R / rpp;
+  p.attn_wgs = B * Hkv * R;
+  const size_t lds = (size_t)nwv * dattn::KB * D * 2 + (size_t)nwv * 16 * D * 4 + (size_t)2 * nwv * 16 * 4;
+  const dim3 grid(p.attn_wgs), block(nt);
+  if (D == 64) {
+    (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<64, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((dattn::attn_kernel<64, 8, true>), grid, block, lds, stream, p);
+  } else {
+    (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<128, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((dattn::attn_kernel<128, 4, true>), grid, block, lds, stream, p);
   }
   return (int)hipGetLastError();
 }

@@ -45,6 +45,12 @@ struct Params {
   const int* cache_idx;   // [M / T] (nullable: identity)
   int Lmax;
   int max_pos;            // rows of the cos/sin tables (positions are clamped into them)
+  // pending residual contribution (fp32 [M, K] / [M, N], e.g. o_proj summed by the fused attention
+  // kernel's atomics): NORM prologue sees x = bf16(x + bf16(xadd)); RESID epilogue first folds
+  // yadd into y exactly as the o_proj RESID epilogue would have (y = bf16(y + bf16(yadd))), then
+  // adds its own product, and zeroes yadd for the next layer.  Both nullable.
+  const float* xadd;
+  float* yadd;
 };
 
 constexpr int U = 4;   // 512-element k-steps per load round
@@ -115,9 +121,16 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
 #pragma unroll
       for (int m = 0; m < MM; ++m) {
         if (m < p.M) {
-          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(p.x + (int64_t)m * p.ldx + k);
+          u32x4_t v = *reinterpret_cast<const u32x4_t*>(p.x + (int64_t)m * p.ldx + k);
           float f[8];
           unpack8(v, f);
+          if (p.xadd) {
+            const f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k);
+            const f32x4_t a1 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k + 4);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = bf2f(f2bf(f[j] + bf2f(f2bf(j < 4 ? a0[j] : a1[j - 4]))));
+            v = pack8(f);
+          }
 #pragma unroll
           for (int j = 0; j < 8; ++j) ss[m] += f[j] * f[j];
           *reinterpret_cast<u32x4_t*>(xs + m * p.K + k) = v;
@@ -252,7 +265,15 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
       for (int r = 0; r < NW; ++r) {
         const int n = wave * NW + r;
         if (n >= p.N) continue;
-        if (EPI == RESID) yr[n] = f2bf(bf2f(yr[n]) + bf2f(f2bf(acc[m][r])));
+        if (EPI == RESID) {
+          float yv = bf2f(yr[n]);
+          if (p.yadd) {
+            float* ya = p.yadd + (int64_t)m * p.N + n;
+            yv = bf2f(f2bf(yv + bf2f(f2bf(*ya))));
+            *ya = 0.f;
+          }
+          yr[n] = f2bf(yv + bf2f(f2bf(acc[m][r])));
+        }
         else yr[n] = f2bf(acc[m][r]);
       }
     }
@@ -320,13 +341,14 @@ void dgemv_set_knob(int which, int value) {
 int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,
                  int64_t ldy, int M, int N, int K, int nq, int nkv, int D, const float* cos_t, const float* sin_t,
                  const int64_t* pos, int T, void* kc, void* vc, int64_t c_sb, int64_t c_sh, int64_t c_sl,
-                 const int* cache_idx, int Lmax, int max_pos, hipStream_t stream) {
+                 const int* cache_idx, int Lmax, int max_pos, const float* xadd, float* yadd, hipStream_t stream) {
   if (M < 1 || M > 8 || N < 1 || K < 8 || (K % 8)) return -1;
+  if ((xadd && !norm_w) || (yadd && epi != dfused::RESID)) return -3;
   if (norm_w && (size_t)M * K * 2 > 65536) return -2;
   dfused::Params p{static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(norm_w), eps,
                    static_cast<const uint16_t*>(w), ldw, static_cast<uint16_t*>(y), ldy, M, N, K, nq, nkv, D, cos_t,
                    sin_t, pos, T, static_cast<uint16_t*>(kc), static_cast<uint16_t*>(vc), c_sb, c_sh, c_sl, cache_idx,
-                   Lmax, max_pos};
+                   Lmax, max_pos, xadd, yadd};
   const bool norm = norm_w != nullptr;
   if (M == 1) return dfused::dispatch<1>(p, epi, norm, stream);
   if (M == 2) return dfused::dispatch<2>(p, epi, norm, stream);

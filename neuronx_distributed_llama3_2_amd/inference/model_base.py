@@ -38,6 +38,9 @@ from ..parallel_layers.parallel_state import get_tensor_model_parallel_size
 # into the Infinity Cache from spare workgroups (0 disables), and how many workgroups do it.
 _PREFETCH_MB = float(os.environ.get("NXD_DECODE_PREFETCH_MB", "0"))
 _PREFETCH_WGS = int(os.environ.get("NXD_DECODE_PREFETCH_WGS", "256"))
+# decode attention + o_proj in one launch (csrc/decode_attn.hip FUSE); the o_proj sum reaches the
+# residual stream through the next two fused GEMVs (xadd / yadd side inputs)
+_ATTN_OPROJ = os.environ.get("NXD_DECODE_ATTN_OPROJ", "1") == "1"
 
 
 class DecoderInferenceMixin:
@@ -165,6 +168,14 @@ class DecoderInferenceMixin:
         lm = self.lm_head.weight
         return lm.dtype == torch.bfloat16 and getattr(self.lm_head, "bias", None) is None
 
+    def _decode_oacc(self, M: int, res: torch.Tensor) -> torch.Tensor:
+        """fp32 [8, H] o_proj accumulator of the fused attention + o_proj decode launch: zero between
+        uses (the down projection's epilogue re-zeroes the rows it consumed)."""
+        buf = getattr(self, "_oacc_buf", None)
+        if buf is None or buf.device != res.device or buf.shape[1] != res.shape[1]:
+            buf = self._oacc_buf = torch.zeros((8, res.shape[1]), dtype=torch.float32, device=res.device)
+        return buf
+
     def _forward_decode_fused(self, input_ids, positions, seq_ids, cache_len, last_index, return_hidden):
         C = ops.ext()
         B, T = input_ids.shape
@@ -191,6 +202,15 @@ class DecoderInferenceMixin:
                 # spare workgroups of the attention launch pull o_proj and the head of gate_up into
                 # the Infinity Cache while the (latency-bound) attention leaves HBM idle
                 C.decode_attn_prefetch(attn.o_proj.weight, -1, w_gu, int(_PREFETCH_MB * 2**20), _PREFETCH_WGS)
+            oacc = self._decode_oacc(M, res) if (_ATTN_OPROJ and _PREFETCH_MB <= 0) else None
+            if oacc is not None and C.decode_attn_oproj(q, kc, vc, sid32, cache_len.to(torch.int32), attn.o_proj.weight,
+                                                        oacc, 1.0 / math.sqrt(D)):
+                # oacc += o_proj(attention) (one launch); the GLU prologue sees res + oacc, the down
+                # epilogue folds it into res with the unfused rounding and zeroes it
+                a = torch.empty((M, w_d.shape[1]), dtype=res.dtype, device=res.device)
+                C.dgemv(2, res, ln2, self.eps, w_gu, a, 0, 0, 0, None, None, None, 1, None, None, None, oacc, None)
+                C.dgemv(1, a, None, 0.0, w_d, res, 0, 0, 0, None, None, None, 1, None, None, None, None, oacc)
+                continue
             o = ops.decode_attention(q, kc, vc, cache_len, sid32)
             C.dgemv(1, o.reshape(M, nq * D), None, 0.0, attn.o_proj.weight, res, 0, 0, 0, None, None, None, 1,
                     None, None, None)                                   # res += o_proj(o)

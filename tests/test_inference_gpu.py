@@ -220,6 +220,45 @@ def test_fused_decode_matches_unfused(hidden, heads):
     assert ((lf - lu).abs().max() / lu.abs().max()).item() < 3e-2
 
 
+@pytest.mark.parametrize("hidden,heads,kv", [(512, 8, 2), (2048, 32, 8), (1024, 8, 2)])   # D = 64, 64, 128
+def test_fused_attention_oproj_matches_two_launches(monkeypatch, hidden, heads, kv):
+    """decode_attn.hip FUSE (attention + o_proj in one launch, o_proj rows added by float atomics
+    into an fp32 accumulator that the GLU prologue / down epilogue fold into the residual) vs the
+    attention launch + RESID o_proj GEMV: same greedy tokens, close logits, accumulator left zero."""
+    from transformers import LlamaConfig, LlamaForCausalLM as HF
+    from neuronx_distributed_llama3_2_amd.inference import model_base
+
+    cfg = LlamaConfig(hidden_size=hidden, intermediate_size=2 * hidden, num_hidden_layers=2, num_attention_heads=heads,
+                      num_key_value_heads=kv, vocab_size=1000, max_position_embeddings=1024, rms_norm_eps=1e-5,
+                      rope_theta=500000.0, tie_word_embeddings=True, eos_token_id=2)
+    torch.manual_seed(0)
+    sd = {k: v.detach().clone() for k, v in HF(cfg).state_dict().items()}
+    torch.manual_seed(5)
+    ids = torch.randint(3, cfg.vocab_size, (2, 33))
+    outs, models = [], []
+    for on in (True, False):
+        monkeypatch.setattr(model_base, "_ATTN_OPROJ", on)
+        m = _model(cfg, sd, torch.bfloat16, graphs=True, steps=4, device=torch.device("cuda"))
+        outs.append(m.generate(ids, max_new_tokens=24, eos_token_id=-1).cpu())
+        models.append(m)
+    assert models[0].model._decode_fused_ok is True
+    buf = getattr(models[0].model, "_oacc_buf", None)
+    assert buf is not None and int((buf != 0).sum()) == 0, "fused path not taken or accumulator not consumed"
+    assert torch.equal(outs[0][:, :45], outs[1][:, :45]) and (outs[0] == outs[1]).float().mean() > 0.95
+    # one decode step on identical caches: logits agree
+    f, u = models[0].model, models[1].model
+    f.kv_cache.copy_(u.kv_cache)
+    last = outs[1][:, -1:].cuda()
+    pos = torch.full((2, 1), outs[1].shape[1] - 1, dtype=torch.int64, device="cuda")
+    sid = torch.arange(2, device="cuda")
+    clen = torch.full((2,), outs[1].shape[1], dtype=torch.int32, device="cuda")
+    monkeypatch.setattr(model_base, "_ATTN_OPROJ", True)
+    lf = f.forward_tokens(last, pos, sid, clen).float()
+    monkeypatch.setattr(model_base, "_ATTN_OPROJ", False)
+    lu = u.forward_tokens(last, pos, sid, clen).float()
+    assert ((lf - lu).abs().max() / lu.abs().max()).item() < 2e-2
+
+
 def test_fused_decode_weight_prefetch_is_exact(monkeypatch):
     """Spare attention workgroups streaming o_proj / gate_up into the Infinity Cache only read:
     decode tokens and logits are bit-identical with and without the prefetch."""
