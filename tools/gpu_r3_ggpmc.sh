@@ -9,3 +9,5 @@ for m in 0 1 2; do
   timeout -s KILL 90 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT -d $D/m${m}_p2 -o run --output-format csv -- python tools/prof_grouped.py $m 3 > $D/m${m}_p2.log 2>&1 || exit $?
 done
 timeout -k 10 300 python -u tools/bench_grouped_gemm.py > $D/grouped_gemm_vs_framework_loop.jsonl 2>&1 || exit $?
+timeout -k 10 900 python bench.py --gpus 1 --steps 4 --warmup 2 --mbs 2 > $D/bench_mbs2.log 2>&1 || exit $?
+timeout -k 10 900 python bench.py --gpus 1 --steps 4 --warmup 2 --mbs 1 > $D/bench_mbs1.log 2>&1 || exit $?
