@@ -1,7 +1,10 @@
 """GEMM-side cost of sequence-parallel chunking (parallel_layers/sp.py) at the per-rank Llama-3-8B
 shapes of TP = 2 / 4 / 8: per-layer time of the chunked column/row forward GEMMs and backward dgrad
 GEMMs for c = 1, 2, 4, 8 chunks (wgrad GEMMs are unchunked and excluded).  The communication side
-of the trade-off needs the multi-GPU run; this isolates what chunking costs the matrix cores."""
+of the trade-off needs the multi-GPU run; this isolates what chunking costs the matrix cores.
+
+    python tools/bench_sp_chunks.py [--tp 8 --mbs 4]   (rows per rank-GEMM = mbs * 8192)"""
+import argparse
 import json
 import sys
 
@@ -23,8 +26,12 @@ def timed(fn, reps=20):
     return s.elapsed_time(e) / reps
 
 
-S, H, I, Q, KV = 8192, 4096, 14336, 4096, 1024
-for tp in (2, 4, 8):
+ap = argparse.ArgumentParser()
+ap.add_argument("--tp", type=int, nargs="+", default=[2, 4, 8])
+ap.add_argument("--mbs", type=int, default=1, help="sequences per micro-batch (GEMM rows = mbs * 8192)")
+a = ap.parse_args()
+S, H, I, Q, KV = 8192 * a.mbs, 4096, 14336, 4096, 1024
+for tp in a.tp:
     # (name, N_out, K_in) of the per-rank weight [N, K]
     col = [("qkv", (Q + 2 * KV) // tp, H), ("gate_up", 2 * I // tp, H)]
     row = [("o", H, Q // tp), ("down", H, I // tp)]
@@ -44,4 +51,4 @@ for tp in (2, 4, 8):
             tot += fwd + bwd
             print(json.dumps({"tp": tp, "chunks": c, "gemm": n, "fwd_ms": round(fwd, 4), "dgrad_ms": round(bwd, 4)}),
                   flush=True)
-        print(json.dumps({"tp": tp, "chunks": c, "layer_fwd_dgrad_ms": round(tot, 4)}), flush=True)
+        print(json.dumps({"tp": tp, "mbs": a.mbs, "chunks": c, "layer_fwd_dgrad_ms": round(tot, 4)}), flush=True)
