@@ -24,9 +24,12 @@
 //   * dQ: dS^T crosses LDS once; each wave computes one 32-wide d block of dS . K over the
 //     block's 256 keys (D=128; D=64 splits keys in halves and sums the halves in LDS) and adds
 //     it with f32 atomics into an fp32 dQ accumulator.  At 256 keys per block the atomic volume
-//     is one byte per 640 FLOPs (half of a 128-key design).  Not a floor: with the atomics,
-//     tile loads and barriers all ablated the body still runs only 839-930 TF/s
-//     (profiles/r2_fab_ablate_after.jsonl).
+//     is one byte per 640 FLOPs (half of a 128-key design).  At S=8192, 32/8 heads that is 2.21 GB
+//     of dQ adds + 0.55 GB of dK/dV adds; at the chip-wide f32 atomic rate (~1.3 TB/s, any adder
+//     placement) that alone is ~2.1 ms, the kernel's time (profiles/r2_fab_ablate_after.jsonl: the
+//     body with every atomic ablated runs 1.59 ms).  Going lower needs fewer atomic BYTES, not a
+//     faster body: 256 keys per workgroup is the register-file maximum for resident dK/dV
+//     (256 keys x 128 d x 2 x 4 B = half of a CU's 512 KiB of registers).
 #include "common.h"
 
 #include <algorithm>
