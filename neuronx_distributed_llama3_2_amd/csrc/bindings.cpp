@@ -68,6 +68,8 @@ int grouped_rowgemm_launch(int, const void*, const void*, void*, const int*, int
 int wgrad_gemm_grouped_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int64_t, const int*, int, int,
                               int, int, hipStream_t);
 void wgrad_gemm_set_ablate(int);
+void grouped_rowgemm_set_pp(int);
+void wgrad_gemm_set_pp(int);
 int cu_stream_launch(const void*, void*, int64_t, int, int64_t, hipStream_t);
 int moe_combine_fwd_launch(const void*, const int64_t*, const float*, void*, int64_t, int, int, hipStream_t);
 int moe_combine_bwd_launch(const void*, const void*, const int64_t*, const float*, void*, float*, int64_t, int, int,
@@ -962,6 +964,9 @@ PYBIND11_MODULE(_C, m) {
              "cu_stream");
   });
   m.def("wgrad_gemm_set_ablate", [](int64_t v) { nxd::wgrad_gemm_set_ablate((int)v); });
+  // ping-pong (staggered wave-group) main loops of the two hand-written GEMMs, for in-process A/B
+  m.def("grouped_rowgemm_set_pp", [](int64_t v) { nxd::grouped_rowgemm_set_pp((int)v); });
+  m.def("wgrad_gemm_set_pp", [](int64_t v) { nxd::wgrad_gemm_set_pp((int)v); });
   m.def("wgrad_gemm_splits", [](int64_t T, int64_t M, int64_t N) { return nxd::wgrad_gemm_choose_splits((int)T, (int)M, (int)N); });
   m.def("moe_combine_fwd", &moe_combine_fwd);
   m.def("moe_combine_bwd", &moe_combine_bwd);

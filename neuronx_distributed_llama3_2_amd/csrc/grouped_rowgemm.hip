@@ -13,8 +13,9 @@
 //   * 8 waves (512 threads), 256 x 256 output tile, one workgroup per CU; waves 2 (M) x 4 (N) of
 //     128 x 64 = 8 x 4 v_mfma_f32_16x16x32_bf16 tiles, 128 fp32 accumulators per lane;
 //   * reduction step BK = 32, 4-stage LDS ring (4 x 32 KiB) filled by LDS-DMA (1 KiB lane-linear
-//     pieces, swizzle applied to the source address), counted vmcnt per stage, one raw barrier per
-//     stage, fragments of stage t+1 read while stage t's 32 MFMAs run;
+//     pieces, swizzle applied to the source address), counted vmcnt; default main loop = the
+//     ping-pong one (PP below: wave groups staggered by one barrier, +3-9 % over one barrier per
+//     stage, bitwise-identical output, profiles/r3_pp_mainloop_ab.jsonl);
 //   * operands consumed along their contiguous axis (A; DGRAD's B) sit in a [256][32] row image
 //     (64-B rows, 16-B chunk c stored at c ^ g[(row >> 2) & 3], g = {0, 2, 3, 1}: every 16-lane
 //     group of a ds_read_b128 fragment read covers all 64 banks once); FWD's B (reduction along its
@@ -93,7 +94,19 @@ __device__ __forceinline__ void wait_vm(int newer) {
 
 // Measured and not kept (profiles/r3_grouped_rowgemm_variants.jsonl): a 5-stage ring (160 KiB) and
 // s_setprio around the MFMA clusters or for the younger wave half -- all within +-2 %.
-template <int MODE>
+//
+// PP (ping-pong): each 32-deep stage is two phases of 16 MFMAs per wave, every phase
+// [LDS-DMA half-stage][fragment reads] barrier [16 MFMAs at raised priority] barrier, and wave group
+// 1 (waves 4-7; every SIMD holds one wave of each group) runs one barrier behind group 0, so on each
+// SIMD one wave's MFMA burst covers the other wave's reads and DMA issue (cdna_hip_programming.md,
+// "The 256^2 8-phase template").  Ring safety, global barrier instances #n (group 0 passes #(4t+2h)
+// and #(4t+2h+1) in phase (t, h); group 1 one later):
+//   * stage S is read from #(4S-1) on (group 0, phase (S, 0)); both groups retire their pieces of S
+//     before arriving there (group 0 after its MFMAs of (S-1, 1), group 1 before its reads of (S-1, 1));
+//   * the last reads of stage S complete before #(4S+4) (group 1's MFMAs of (S, 1)); its slot is
+//     refilled with S+4 after that: group 1 in (S+1, 0/1), group 0 in (S+1, 1) and (S+2, 0);
+//   * pieces issued after stage S's last: S+1 (4) and S+2's first half (2) -> vmcnt(6), less at the tail.
+template <int MODE, bool PP>
 __global__ void __launch_bounds__(NT, 1) rowgemm_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int id = xcd_remap(blockIdx.x, gridDim.x);
@@ -167,6 +180,69 @@ __global__ void __launch_bounds__(NT, 1) rowgemm_kernel(Params p) {
   };
   auto bfrag = [&](const char* img, int c0) { return MODE == FWD ? frag_tr(img, c0) : frag_row(img, c0); };
 
+  if constexpr (PP) {
+    const int grp = wm;
+    auto issue_half = [&](int s, int hh) {
+      if (s >= nk) return;
+      const uint32_t img = lds0 + (s % STAGES) * STAGE_BYTES + wid * PIECES * 1024;
+      const int oa = s * BK;
+      const int64_t ob = MODE == FWD ? (int64_t)s * BK * p.ldb : (int64_t)s * BK;
+      dma16(src_a[hh] + oa, __builtin_amdgcn_readfirstlane(img + hh * 1024));
+      dma16(src_b[hh] + ob, __builtin_amdgcn_readfirstlane(img + IMG_BYTES + hh * 1024));
+    };
+    auto wait_stage = [&](int S) {   // this thread's pieces of stage S landed
+      if (S + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (S + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    auto barrier = [] {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    issue_half(0, 0); issue_half(0, 1); issue_half(1, 0); issue_half(1, 1); issue_half(2, 0);
+    wait_stage(0);
+    if (grp == 1) issue_half(2, 1);
+    barrier();
+    if (grp == 1) barrier();   // the stagger
+    bf16x8_t af[4], bf[4];
+    for (int t = 0; t < nk; ++t) {
+      const char* img = smem + (t % STAGES) * STAGE_BYTES;
+      // ---- phase (t, 0): B fragments + A rows 0..63 of the wave
+      if (grp == 0) issue_half(t + 2, 1); else issue_half(t + 3, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = bfrag(img + IMG_BYTES, wn * 64 + 16 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag_row(img, wm * 128 + 16 * i);
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      // ---- phase (t, 1): A rows 64..127
+      if (grp == 1) {
+        if (t + 1 < nk) wait_stage(t + 1);
+        issue_half(t + 3, 1);
+      } else {
+        issue_half(t + 3, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag_row(img, wm * 128 + 16 * (4 + i));
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (grp == 0 && t + 1 < nk) wait_stage(t + 1);
+      barrier();
+    }
+    if (grp == 0) barrier();   // equal barrier counts before the epilogue's __syncthreads
+  } else {
   for (int s = 0; s < STAGES - 1 && s < nk; ++s) issue(s);
   bf16x8_t af[8], bf[4];
   if (nk > 0) {
@@ -194,6 +270,7 @@ __global__ void __launch_bounds__(NT, 1) rowgemm_kernel(Params p) {
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) bf[j] = bn[j];
+  }
   }
 
   // ---- epilogue: 4 rounds of 32 rows x 64 columns per wave through a padded LDS slab, then bf16
@@ -225,6 +302,15 @@ __global__ void __launch_bounds__(NT, 1) rowgemm_kernel(Params p) {
   }
 }
 
+static int g_pp = -1;   // ping-pong variant (NXD_GRG_PP; settable for in-process A/B)
+static bool use_pp() {
+  if (g_pp < 0) {
+    const char* e = getenv("NXD_GRG_PP");
+    g_pp = e ? (atoi(e) != 0) : 1;
+  }
+  return g_pp != 0;
+}
+
 static int band_rows() {
   static const int b = [] {
     const char* e = getenv("NXD_GRG_BAND");   // 8: +2..7 % over 4 on most Mixtral shapes (r3_grouped_rowgemm_variants)
@@ -235,6 +321,8 @@ static int band_rows() {
 }
 
 }  // namespace grg
+
+void grouped_rowgemm_set_pp(int v) { grg::g_pp = v != 0; }
 
 // mode 0 FWD:   a = x [rows, K],  W [E, K, N], c = y  [rows, N]
 // mode 1 DGRAD: a = dy [rows, N], W [E, K, N], c = dx [rows, K]
@@ -266,10 +354,14 @@ int grouped_rowgemm_launch(int mode, const void* a, const void* w, void* c, cons
   p.band = grg::band_rows();
   const int64_t nwg = (int64_t)p.rt * p.nt;
   if (nwg > INT32_MAX) return -2;
-if (mode == grg::FWD)
-    hipLaunchKernelGGL(grg::rowgemm_kernel<grg::FWD>, dim3((unsigned)nwg), dim3(grg::NT), 0, stream, p);
-  else
-    hipLaunchKernelGGL(grg::rowgemm_kernel<grg::DGRAD>, dim3((unsigned)nwg), dim3(grg::NT), 0, stream, p);
+  const bool pp = grg::use_pp();
+  if (mode == grg::FWD) {
+    if (pp) hipLaunchKernelGGL((grg::rowgemm_kernel<grg::FWD, true>), dim3((unsigned)nwg), dim3(grg::NT), 0, stream, p);
+    else hipLaunchKernelGGL((grg::rowgemm_kernel<grg::FWD, false>), dim3((unsigned)nwg), dim3(grg::NT), 0, stream, p);
+  } else {
+    if (pp) hipLaunchKernelGGL((grg::rowgemm_kernel<grg::DGRAD, true>), dim3((unsigned)nwg), dim3(grg::NT), 0, stream, p);
+    else hipLaunchKernelGGL((grg::rowgemm_kernel<grg::DGRAD, false>), dim3((unsigned)nwg), dim3(grg::NT), 0, stream, p);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -22,6 +22,8 @@
 //     (global_load_lds_dwordx4, lane-linear 1 KiB pieces) while stage t is consumed, each wave
 //     waits with a COUNTED vmcnt for its own pieces of stage t only, and one raw s_barrier per
 //     stage publishes it (no vmcnt(0) in the loop: two stages stay in flight across every barrier);
+//     default: the ping-pong variant of that loop (two 16-MFMA phases per stage, wave groups one
+//     barrier apart; +3-16 %, profiles/r3_pp_mainloop_ab.jsonl);
 //   * LDS image of an operand stage: [32 tokens][256 features], 512-B rows, 16-B chunk c stored at
 //     c ^ 2 * ((t & 3) | ((t >> 3) & 1) << 2): the two 16-lane groups of a transposed read (4 token
 //     rows x 16 features each, rows t, t + 8) land on 16 distinct bank quads — conflict-free.  The
@@ -103,7 +105,9 @@ __device__ __forceinline__ void wait_vm(int newer) {   // this thread's pieces o
 
 // s_setprio around the MFMA clusters or for the younger wave half measured within +-2 % (not kept,
 // profiles/r3_wgrad_kernel_prio_rejected.jsonl)
-template <bool GROUPED>
+// PP: the ping-pong main loop of csrc/grouped_rowgemm.hip (two 16-MFMA phases per stage, wave group
+// 1 one barrier behind group 0; ring-safety argument there).
+template <bool GROUPED, bool PP>
 __global__ void __launch_bounds__(NT, 1) wgrad_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int tiles = p.mt * p.nt;
@@ -185,6 +189,70 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(Params p) {
   // MFMA; B fragments into a second set) -- the MFMA pipe never waits on an LDS read after a
   // barrier.  LDS-DMA: stages t+1 .. t+3 in flight at most; a stage is waited for two iterations
   // after its issue.
+  if constexpr (PP) {
+    const int grp = wm;
+    auto issue_half = [&](int s, int hh) {
+      if (s >= nk || (p.ablate & 4 && s >= STAGES - 1)) return;
+      const uint32_t img = lds0 + (s % STAGES) * STAGE_BYTES + wid * PIECES * 1024;
+      const uint16_t* sa = src_a[hh] + (int64_t)s * BK * p.ld_dy;
+      const uint16_t* sb = src_b[hh] + (int64_t)s * BK * p.ld_x;
+      if constexpr (GROUPED) {
+        if (s * BK + tt_of[hh] >= rows) sa = sb = reinterpret_cast<const uint16_t*>(g_zero16);
+      }
+      dma16(sa, __builtin_amdgcn_readfirstlane(img + hh * 1024));
+      dma16(sb, __builtin_amdgcn_readfirstlane(img + IMG_BYTES + hh * 1024));
+    };
+    auto wait_stage = [&](int S) {
+      if (S + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (S + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    auto barrier = [] {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    issue_half(0, 0); issue_half(0, 1); issue_half(1, 0); issue_half(1, 1); issue_half(2, 0);
+    wait_stage(0);
+    if (grp == 1) issue_half(2, 1);
+    barrier();
+    if (grp == 1) barrier();   // the stagger
+    bf16x8_t af[4], bf[4];
+    for (int t = 0; t < nk; ++t) {
+      const char* img = smem + (t % STAGES) * STAGE_BYTES;
+      if (grp == 0) issue_half(t + 2, 1); else issue_half(t + 3, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = frag(img + IMG_BYTES, wn * 64 + 16 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag(img, wm * 128 + 16 * i);
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      if (grp == 1) {
+        if (t + 1 < nk) wait_stage(t + 1);
+        issue_half(t + 3, 1);
+      } else {
+        issue_half(t + 3, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag(img, wm * 128 + 16 * (4 + i));
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (grp == 0 && t + 1 < nk) wait_stage(t + 1);
+      barrier();
+    }
+    if (grp == 0) barrier();
+  } else {
   for (int s = 0; s < STAGES - 1 && s < nk; ++s) issue(s);
   bf16x8_t af[8], bf[4];
   if (nk > 0) {
@@ -218,6 +286,7 @@ __global__ void __launch_bounds__(NT, 1) wgrad_kernel(Params p) {
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) bf[j] = bn[j];
+  }
   }
 
   // ---- epilogue: per wave, 4 rounds of 32 rows x 64 columns through a private padded LDS slab
@@ -259,14 +328,27 @@ static int band_rows() {
 
 static int g_ablate = 0;
 
+static int g_pp = -1;   // ping-pong main loop (NXD_WG_PP; settable for in-process A/B)
+static bool use_pp() {
+  if (g_pp < 0) {
+    const char* e = getenv("NXD_WG_PP");
+    g_pp = e ? (atoi(e) != 0) : 1;
+  }
+  return g_pp != 0;
+}
+
 template <bool G>
 void launch(const Params& p, int64_t nwg, hipStream_t stream) {
-  hipLaunchKernelGGL((wgrad_kernel<G>), dim3((unsigned)nwg), dim3(NT), 0, stream, p);
+  if (use_pp())
+    hipLaunchKernelGGL((wgrad_kernel<G, true>), dim3((unsigned)nwg), dim3(NT), 0, stream, p);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<G, false>), dim3((unsigned)nwg), dim3(NT), 0, stream, p);
 }
 
 }  // namespace wg
 
 void wgrad_gemm_set_ablate(int v) { wg::g_ablate = v; }
+void wgrad_gemm_set_pp(int v) { wg::g_pp = v != 0; }
 
 // Token splits per output tile.  Cost model in token steps (BK = 32) of one workgroup: grid waves
 // of 256 workgroups x (steps per split + ~10 for the atomic epilogue); the smallest split count

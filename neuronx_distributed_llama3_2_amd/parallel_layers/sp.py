@@ -36,13 +36,17 @@ from .parallel_state import get_tensor_model_parallel_group
 
 _SP_CHUNKS = int(os.environ["NXD_SP_CHUNKS"]) if "NXD_SP_CHUNKS" in os.environ else None
 
-# Default chunk count per TP degree.  Chunking trades exposed communication for smaller GEMMs;
-# profiles/r1_sp_chunks_gemm.jsonl (tools/bench_sp_chunks.py) measures the GEMM side per layer
-# (fwd + dgrad, Llama-3-8B, S=8192): TP8 0.74 / 0.83 / 1.13 ms and TP2 2.58 / 2.57 / 2.99 ms for
-# c = 1 / 2 / 4.  With a ring collective of time T per op the exposed part is ~max(T + g/c,
-# T/c + g) - g; over the plausible xGMI range (T = 70-300 us at TP8) c=2 beats c=4 at TP8 by
-# >= 120 us per layer, while TP2 (one link pair, T ~ 440 us) still prefers c=4.
-_DEFAULT_CHUNKS = {2: 4, 4: 2, 8: 2}
+# Default chunk count per TP degree, for the micro-batch bench.py runs each degree at (MBS_BY_TP:
+# 2 sequences at TP2, 4 at TP4 / TP8).  Chunking trades exposed communication (the first gather /
+# last reduce-scatter of each op, ~T/c) for smaller GEMMs.  GEMM side per layer (fwd + dgrad,
+# Llama-3-8B, S=8192, tools/bench_sp_chunks.py, profiles/r3_sp_chunks_gemm_mbs.jsonl), c = 1/2/4/8:
+# TP8 mbs 4: 2.67 / 2.68 / 2.80 / 3.20 ms; TP4 mbs 4: 4.90 / 4.97 / 5.09 / 5.32; TP2 mbs 2: 4.81 /
+# 4.84 / 4.97 / 5.83.  Going from c=2 to c=4 costs 0.12-0.13 ms per layer and saves ~T/4 on each
+# of the ~3 exposed collective ends per layer, T = one 32k-token (256 MiB) SP all-gather or
+# reduce-scatter: a win for any T above ~0.17 ms, i.e. below ~1.3 TB/s of ring bandwidth -- every
+# plausible xGMI figure.  c=8 costs 0.5 ms per layer at TP8 and is not worth it.  (At micro-batch 1
+# the GEMMs are 4x smaller and chunking costs relatively more: profiles/r1_sp_chunks_gemm.jsonl.)
+_DEFAULT_CHUNKS = {2: 4, 4: 4, 8: 4}
 
 
 def set_sequence_parallel_chunks(c: Optional[int]) -> None:
