@@ -83,13 +83,17 @@ def _use_wgrad_t(go2: torch.Tensor, x2: torch.Tensor = None, K: int = None) -> b
 # 5-13 % slower than the bare TN GEMM on the large TP=1 shapes.  Counting the TN path's two operand
 # transposes the isolated kernel should also win TP=1 qkv / o_proj, but inside the TP=1 step that
 # routing measured +4.6 ms per 2 micro-batches (GEMM + wgrad kernel + transposes 531.9 vs 527.3 ms,
-# profiles/r3_step_breakdown_wgrad_all_nocopy_rejected.txt), so `auto` keeps the skinny rule.
+# profiles/r3_step_breakdown_wgrad_all_nocopy_rejected.txt), so `auto` keeps the skinny rule.  With
+# the ping-pong main loop (profiles/r3_wgrad_pp_vs_hipblaslt.jsonl) the kernel also takes the
+# vocabulary-sized output (lm_head) when no producer wrote a feature-major copy: TP=8 1201 vs 1074
+# TF/s for the hipBLASLt path and its two transposes (the 1 GiB logits gradient), TP=1 a tie.
 # NXD_WGRAD_KERNEL = auto | 1 (whenever the shapes allow) | 0.
 _WG_KERNEL = os.environ.get("NXD_WGRAD_KERNEL", "auto")
 _WG_SKINNY = 1100.0
+_WG_WIDE = 16000
 
 
-def _use_wgrad_kernel(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor) -> bool:
+def _use_wgrad_kernel(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor, has_copy: bool = False) -> bool:
     if _WG_KERNEL == "0" or x2 is None or not _native(go2, x2) or mg.dtype != torch.float32:
         return False
     T, M = go2.shape
@@ -98,7 +102,7 @@ def _use_wgrad_kernel(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor) -> 
         return False
     if go2.stride(0) % 8 or x2.stride(0) % 8 or go2.data_ptr() % 16 or x2.data_ptr() % 16:
         return False
-    return _WG_KERNEL == "1" or M * N / (M + N) < _WG_SKINNY
+    return _WG_KERNEL == "1" or M * N / (M + N) < _WG_SKINNY or (not has_copy and max(M, N) >= _WG_WIDE)
 
 
 def _wgrad_scratch(n: int, dtype, device, tag: str = "") -> torch.Tensor:
@@ -121,7 +125,7 @@ def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2, go_t: torch.Tenso
     into a reused scratch, then an fp32 add (the per-micro-batch weight gradient is rounded to
     bf16 before the fp32 accumulation — the precision of the reference's XLA matmul + fp32
     grad accumulation; hipBLASLt's bf16-output solutions run faster than its fp32-output ones)."""
-    if _use_wgrad_kernel(mg, go2, x2):
+    if _use_wgrad_kernel(mg, go2, x2, has_copy=go_t is not None or x_t is not None):
         ext().wgrad_gemm(mg, go2, x2, 0)
         return
     if x_t is not None and not (x_t.dim() == 2 and x_t.is_contiguous() and x_t.shape[1] == go2.shape[0]):

@@ -55,18 +55,20 @@ def test_wgrad_gemm_rejects_bad_shapes():
 
 
 def test_framework_wgrad_dispatch_takes_kernel_on_skinny_shards():
-    """ops.gemm.wgrad_accumulate_ routes the TP=8-like skinny shards (q|k|v: 768 x 4096) to the
-    hand-written kernel and keeps hipBLASLt for the large TP=1 shapes; both accumulate correctly."""
+    """ops.gemm.wgrad_accumulate_ routes the TP=8-like skinny shards (q|k|v: 768 x 4096) and the
+    vocabulary-wide lm_head shard without producer copies (16032 x 4096) to the hand-written kernel
+    and keeps hipBLASLt for the large TP=1 shapes; both accumulate correctly."""
     from neuronx_distributed_llama3_2_amd.ops import gemm as G
 
     torch.manual_seed(1)
     for (T, M, N, copy, want) in [(512, 768, 4096, False, True), (512, 4096, 4096, False, False),
-                                  (512, 4096, 4096, True, False)]:
+                                  (512, 4096, 4096, True, False), (256, 16032, 4096, False, True),
+                                  (256, 16032, 4096, True, False)]:
         dy = torch.randn(T, M, device="cuda", dtype=torch.bfloat16)
         x = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
         mg = torch.randn(M, N, device="cuda", dtype=torch.float32)
         go_t = dy.t().contiguous() if copy else None   # as the SwiGLU backward writes it
-        assert G._use_wgrad_kernel(mg, dy, x) == (want and G._WG_KERNEL != "0")
+        assert G._use_wgrad_kernel(mg, dy, x, has_copy=copy) == (want and G._WG_KERNEL != "0")
         ref = mg.double() + dy.double().t() @ x.double()
         G.wgrad_accumulate_(mg, dy, x, go_t=go_t)
         scale = dy.double().abs().t() @ x.double().abs()
