@@ -18,6 +18,8 @@
 // elements, negligible next to the weights) and read back by every wave with ds_read_b128.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace nxd {
 namespace dfused {
 
@@ -51,6 +53,9 @@ struct Params {
   // adds its own product, and zeroes yadd for the next layer.  Both nullable.
   const float* xadd;
   float* yadd;
+  int pf;                 // issue the epilogue's / prologue's own global reads (residual row, yadd,
+                          // position + cos/sin, RMSNorm weight) at kernel start, next to the first
+                          // weight round, instead of as dependent round trips after the GEMV
 };
 
 constexpr int U = 4;   // 512-element k-steps per load round
@@ -113,6 +118,36 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
   };
   load_round(kbeg);
 
+  // ---- early epilogue / prologue operands (p.pf): independent of the activations, so their
+  // latency overlaps the first weight round instead of following the reduction
+  u32x4_t gw0 = {0, 0, 0, 0};
+  if (NORM && p.pf && tid * 8 < p.K) gw0 = *reinterpret_cast<const u32x4_t*>(p.norm_w + tid * 8);
+  float y_pre[MM][NW], ya_pre[MM][NW];
+  float cs_pre[MM], sn_pre[MM];
+  if (p.pf && lane == 0 && active) {
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+      if (m >= p.M) continue;
+      if (EPI == RESID) {
+#pragma unroll
+        for (int r = 0; r < NW; ++r) {
+          const int n = min(wave * NW + r, p.N - 1);
+          y_pre[m][r] = bf2f(p.y[(int64_t)m * p.ldy + n]);
+          ya_pre[m][r] = p.yadd ? p.yadd[(int64_t)m * p.N + n] : 0.f;
+        }
+      } else if (EPI == ROPE_KV) {
+        const int half = p.D / 2;
+        if (rows[0] < (p.nq + p.nkv) * p.D && rows[1] == rows[0] + half) {
+          const int64_t ps = p.pos[m];
+          const int64_t pt = ps < 0 ? 0 : (ps >= p.max_pos ? p.max_pos - 1 : ps);
+          const int d = rows[0] % p.D;
+          cs_pre[m] = p.cos_t[pt * half + d];
+          sn_pre[m] = p.sin_t[pt * half + d];
+        }
+      }
+    }
+  }
+
   if (NORM) {
     float ss[MM];
 #pragma unroll
@@ -148,7 +183,7 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
     for (int m = 0; m < MM; ++m) rstd[m] = rsqrtf((red[0][m] + red[1][m] + red[2][m] + red[3][m]) / (float)p.K + p.eps);
     for (int k = tid * 8; k < p.K; k += 256 * 8) {
       float g[8];
-      unpack8(*reinterpret_cast<const u32x4_t*>(p.norm_w + k), g);
+      unpack8(p.pf && k == tid * 8 ? gw0 : *reinterpret_cast<const u32x4_t*>(p.norm_w + k), g);
 #pragma unroll
       for (int m = 0; m < MM; ++m) {
         if (m < p.M) {
@@ -239,7 +274,8 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
       if (rows[0] < qk_rows && rows[1] == rows[0] + half) {
         const int h = rows[0] / p.D, d = rows[0] % p.D;
         const int64_t pt = ps < 0 ? 0 : (ps >= p.max_pos ? p.max_pos - 1 : ps);
-        const float c = p.cos_t[pt * half + d], sn = p.sin_t[pt * half + d];
+        const float c = p.pf ? cs_pre[m] : p.cos_t[pt * half + d];
+        const float sn = p.pf ? sn_pre[m] : p.sin_t[pt * half + d];
         const float x1 = bf2f(f2bf(acc[m][0])), x2 = bf2f(f2bf(acc[m][1]));   // bf16 projection output
         const uint16_t o1 = f2bf(x1 * c - x2 * sn), o2 = f2bf(x2 * c + x1 * sn);
         yr[rows[0]] = o1;
@@ -266,10 +302,10 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
         const int n = wave * NW + r;
         if (n >= p.N) continue;
         if (EPI == RESID) {
-          float yv = bf2f(yr[n]);
+          float yv = p.pf ? y_pre[m][r] : bf2f(yr[n]);
           if (p.yadd) {
             float* ya = p.yadd + (int64_t)m * p.N + n;
-            yv = bf2f(f2bf(yv + bf2f(f2bf(*ya))));
+            yv = bf2f(f2bf(yv + bf2f(f2bf(p.pf ? ya_pre[m][r] : *ya))));
             *ya = 0.f;
           }
           yr[n] = f2bf(yv + bf2f(f2bf(acc[m][r])));
@@ -284,6 +320,7 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
 // elements (o_proj 2048 x 2048 -> 2, down 2048 x 8192 -> 4, gate_up / lm_head -> 1)
 int g_glu_pairs = 1;   // knob 0: (gate, up) row pairs per wave of the GLU projection (1 | 2)
 int g_ks = 0;          // knob 1: k-slices per row group (0 = pick_ks)
+int g_pf = -1;         // knob 2: early epilogue / prologue reads (Params::pf; NXD_DECODE_EPI_PF, default 1)
 
 static int pick_ks(int groups, int K) {
   if (g_ks == 1 || g_ks == 2 || g_ks == 4) return g_ks;
@@ -336,6 +373,7 @@ static int dispatch(const Params& p, int epi, bool norm, hipStream_t s) {
 void dgemv_set_knob(int which, int value) {
   if (which == 0) dfused::g_glu_pairs = value == 2 ? 2 : 1;
   else if (which == 1) dfused::g_ks = value;
+  else if (which == 2) dfused::g_pf = value != 0;
 }
 
 int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,
@@ -348,7 +386,12 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
   dfused::Params p{static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(norm_w), eps,
                    static_cast<const uint16_t*>(w), ldw, static_cast<uint16_t*>(y), ldy, M, N, K, nq, nkv, D, cos_t,
                    sin_t, pos, T, static_cast<uint16_t*>(kc), static_cast<uint16_t*>(vc), c_sb, c_sh, c_sl, cache_idx,
-                   Lmax, max_pos, xadd, yadd};
+                   Lmax, max_pos, xadd, yadd, 1};
+  if (dfused::g_pf < 0) {
+    const char* e = getenv("NXD_DECODE_EPI_PF");
+    dfused::g_pf = e ? (atoi(e) != 0) : 1;
+  }
+  p.pf = dfused::g_pf;
   const bool norm = norm_w != nullptr;
   if (M == 1) return dfused::dispatch<1>(p, epi, norm, stream);
   if (M == 2) return dfused::dispatch<2>(p, epi, norm, stream);
