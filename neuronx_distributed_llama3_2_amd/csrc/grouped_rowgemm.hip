@@ -106,6 +106,9 @@ __device__ __forceinline__ void wait_vm(int newer) {
 //   * the last reads of stage S complete before #(4S+4) (group 1's MFMAs of (S, 1)); its slot is
 //     refilled with S+4 after that: group 1 in (S+1, 0/1), group 0 in (S+1, 1) and (S+2, 0);
 //   * pieces issued after stage S's last: S+1 (4) and S+2's first half (2) -> vmcnt(6), less at the tail.
+// Measured and not kept: the LDS-DMA issued inside the MFMA bursts instead of the load phases
+// (vmcnt(8) / (6) by group) -- 1-5 % slower than this on every MoE / dense shape
+// (profiles/r3_pp_dma_in_mfma_rejected.jsonl).
 template <int MODE, bool PP>
 __global__ void __launch_bounds__(NT, 1) rowgemm_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];

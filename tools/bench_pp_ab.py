@@ -2,7 +2,8 @@
 one-barrier-per-stage loop of the two hand-written GEMMs: the grouped MoE row GEMM
 (csrc/grouped_rowgemm.hip, Mixtral-8x7B shapes) and the token-major weight-gradient kernel
 (csrc/wgrad_gemm.hip, dense Llama-3-8B TP=1 / TP=8 shards and grouped MoE).  Interleaved rounds in
-one process; each line also reports the max relative difference of the PP output to the old one."""
+one process; each line also reports the max relative difference of each PP output to the old one.
+v0 = one barrier per stage, v1 = ping-pong with the LDS-DMA issued in the load phase."""
 import json
 import os
 import sys
@@ -25,25 +26,31 @@ def timed(fn, reps):
     return s.elapsed_time(e) / reps
 
 
+VARIANTS = (0, 1)   # one barrier per stage | ping-pong (a third, DMA inside the MFMA burst, was measured and
+                    # dropped: profiles/r3_pp_dma_in_mfma_rejected.jsonl)
+
+
 def ab(kname, fl, fn, out, setter, reps=10, rounds=3, zero=False, **info):
     outs = {}
-    for v in (0, 1):
+    for v in VARIANTS:
         setter(v)
         if zero:
             out.zero_()
         fn()
         torch.cuda.synchronize()
         outs[v] = out.float().clone()
-    t = {0: [], 1: []}
+    t = {v: [] for v in VARIANTS}
     for _ in range(rounds):
-        for v in (0, 1):
+        for v in VARIANTS:
             setter(v)
             t[v].append(timed(fn, reps))
-    setter(0)
+    setter(1)
     ref = outs[0]
-    rel = float((outs[1] - ref).abs().max() / ref.abs().max().clamp(min=1e-30))
-    res = {"kernel": kname, **info, "old_tf": round(fl / min(t[0]) / 1e9, 1), "pp_tf": round(fl / min(t[1]) / 1e9, 1),
-           "old_ms": round(min(t[0]), 4), "pp_ms": round(min(t[1]), 4), "max_rel_diff": rel}
+    res = {"kernel": kname, **info}
+    for v in VARIANTS:
+        res[f"v{v}_tf"] = round(fl / min(t[v]) / 1e9, 1)
+    for v in VARIANTS[1:]:
+        res[f"v{v}_max_rel_diff"] = float((outs[v] - ref).abs().max() / ref.abs().max().clamp(min=1e-30))
     print(json.dumps(res), flush=True)
     return res
 
