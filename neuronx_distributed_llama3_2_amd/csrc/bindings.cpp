@@ -12,7 +12,7 @@ namespace nxd {
 int flash_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, const int64_t*,
                           const int64_t*, const int64_t*, int, int, int, int, int, int, float, int, int,
                           const DropoutArgs&, hipStream_t);
-int64_t flash_attn_bwd_workspace(int, int, int, int, int, int);
+int64_t flash_attn_bwd_workspace(int, int, int, int, int, int, int, int);
 void flash_attn_bwd_set_knob(int, int);
 int transpose_bf16_launch(const void*, void*, int64_t, int64_t, int64_t, int64_t, hipStream_t);
 int flash_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*, float*,
@@ -160,7 +160,7 @@ void flash_attn_bwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == (int64_t)B * Hq * Sq, "bad lse");
   auto opts = q.options().dtype(at::kFloat);
   // fp32 workspace: dQ / dK / dV accumulators + per-row constants (sized by the kernel TU)
-  at::Tensor ws = at::empty({nxd::flash_attn_bwd_workspace(B, Sq, Sk, Hq, Hkv, D)}, opts);
+  at::Tensor ws = at::empty({nxd::flash_attn_bwd_workspace(B, Sq, Sk, Hq, Hkv, D, causal ? 1 : 0, (int)causal_offset)}, opts);
   check_rc(nxd::flash_attn_bwd_launch(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                                       lse.data_ptr<float>(), ws.data_ptr<float>(), dq.data_ptr(),
                                       dk.data_ptr(), dv.data_ptr(), qs, ks, vs, os, dos, dqs, dks, dvs, B, Sq, Sk, Hq, Hkv, D,

@@ -9,8 +9,8 @@
 //   * Work items = (key block, chunk): the host sizes chunks so there are >= 2 items per CU even
 //     at TP=8 head counts (one kv head per GPU), and the causal triangle is cut into near-equal
 //     pieces instead of one workgroup per key block whose runtime is the longest sweep.  Items
-//     of one key block add their dK/dV partials with f32 atomics (~256 KiB per item, small next
-//     to dQ's atomics) into an fp32 workspace a tiny pass narrows to bf16.
+//     of one key block write their dK/dV partials (256 KiB per item) with plain stores into
+//     per-item slabs that the bf16 convert pass sums (f32 atomics into one accumulator: knob 5).
 //   * "key on the lane": S = Q K^T and dP = dO V^T put the key on the MFMA column, so their
 //     fp32 accumulators convert in place into the A operands of dV += P^T dO and dK += dS^T Q
 //     (accumulator-as-operand: no LDS round trip for P / dS), and the dV / dK accumulators come
@@ -59,6 +59,8 @@ struct BwdParams {
   float* dq_acc;        // [B, Hq, Sq_pad, D] fp32, zero-initialised
   float* dk_acc;        // [B, Hkv, Sk_pad, D] fp32, zero-initialised
   float* dv_acc;        // [B, Hkv, Sk_pad, D] fp32, zero-initialised
+  float* dk_slab;       // slab mode (non-null): [B*Hkv, items per bh, kBlockK, D] fp32 per-item partials,
+  float* dv_slab;       //   plain stores (no atomics), summed by slab_convert_kernel
   int64_t q_sb, q_ss, q_sh;
   int64_t k_sb, k_ss, k_sh;
   int64_t v_sb, v_ss, v_sh;
@@ -176,6 +178,7 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
   const int L = p.xcd_map == 2 ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   const int bh = L % BH;
   int kc = L / BH;
+  const int64_t slab = (int64_t)bh * (gridDim.x / BH) + kc;  // this item's dK/dV slab (slab mode)
   // ---- decode (key block, chunk) of this work item: key blocks in order (heaviest first)
   const int nkb = (p.Sk + kBlockK - 1) / kBlockK;
   int kb = 0, it_begin = 0, it_end = 0;
@@ -190,7 +193,15 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
     }
     kc -= nc;
   }
-  if (kb >= nkb || it_begin >= it_end) return;  // (host sizes the grid exactly; defensive)
+  if (kb >= nkb || it_begin >= it_end) {  // (host sizes the grid exactly; defensive)
+    if (p.dk_slab != nullptr) {  // an empty item's slab still enters the sum
+      for (int i = threadIdx.x; i < kBlockK * D; i += kThreads) {
+        p.dk_slab[slab * kBlockK * D + i] = 0.f;
+        p.dv_slab[slab * kBlockK * D + i] = 0.f;
+      }
+    }
+    return;
+  }
 
   const int b = bh / p.Hkv, hkv = bh % p.Hkv;
   const int Sq_pad = (p.Sq + kBlockQ - 1) / kBlockQ * kBlockQ;
@@ -574,6 +585,32 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
   // the dK/dV MFMAs are inline asm (invisible to the hazard recognizer): give the last ones their
   // pass latency before the accumulators are read
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  if (p.dk_slab != nullptr) {
+    // slab mode: this item's dK / dV partials -> its own slab with plain stores (every column,
+    // untouched ones as zeros; the accumulators of a fully masked column stay 0)
+    if (p.ablate & 2) return;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int64_t srow0 = slab * kBlockK + 64 * w + 32 * c;
+#pragma unroll
+      for (int dbk = 0; dbk < NDB; ++dbk) {
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          int64_t off = (srow0 + 8 * gq + 4 * hh) * D + 32 * dbk + r;
+          asm volatile("" : "+v"(off));
+          float* dkr = p.dk_slab + off;
+          float* dvr = p.dv_slab + off;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            dkr[i * D] = acc_dk[c][dbk][4 * gq + i];
+            dvr[i * D] = acc_dv[c][dbk][4 * gq + i];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    return;
+  }
   // ---- dK, dV partials -> fp32 workspace: C rows = key, col = d (d on the lane)
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
@@ -649,6 +686,47 @@ __global__ void __launch_bounds__(256) acc_convert_kernel(const float* acc, uint
   float f[8] = {a0[0] * scale, a0[1] * scale, a0[2] * scale, a0[3] * scale,
                 a1[0] * scale, a1[1] * scale, a1[2] * scale, a1[3] * scale};
   *reinterpret_cast<u32x4_t*>(out + b * sb + (int64_t)si * ss + h * sh + c * 8) = pack8(f);
+}
+
+// slab mode: out (bf16, strided [B,S,H,D]) = scale * sum of the per-item partials of the row's
+// key block (items of key block kb of one (b, h) are slabs [pre(kb), pre(kb) + nc(kb)) of that
+// (b, h): the kernel's item numbering)
+template <int D>
+__global__ void __launch_bounds__(256) slab_convert_kernel(const float* slab, uint16_t* out, int64_t sb, int64_t ss,
+                                                          int64_t sh, int B, int S, int H, float scale, int Sq, int G,
+                                                          int causal, int coff, int chunk, int per_bh) {
+  constexpr int LPR = D / 8;
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
+  const int c = threadIdx.x % LPR;
+  const int64_t nrows = (int64_t)B * H * S;
+  if (row >= nrows) return;
+  const int b = row / ((int64_t)H * S);
+  const int h = (row / S) % H;
+  const int si = row % S;
+  const int kb = si / kBlockK;
+  int pre = 0;
+  for (int k2 = 0; k2 < kb; ++k2) pre += (kb_iters(k2, Sq, G, causal, coff) + chunk - 1) / chunk;
+  const int nc = (kb_iters(kb, Sq, G, causal, coff) + chunk - 1) / chunk;
+  const float* sp = slab + (((int64_t)(b * H + h) * per_bh + pre) * kBlockK + si % kBlockK) * D + c * 8;
+  f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < nc; ++j) {
+    a0 += *reinterpret_cast<const f32x4_t*>(sp + (int64_t)j * kBlockK * D);
+    a1 += *reinterpret_cast<const f32x4_t*>(sp + (int64_t)j * kBlockK * D + 4);
+  }
+  float f[8] = {a0[0] * scale, a0[1] * scale, a0[2] * scale, a0[3] * scale,
+                a1[0] * scale, a1[1] * scale, a1[2] * scale, a1[3] * scale};
+  *reinterpret_cast<u32x4_t*>(out + b * sb + (int64_t)si * ss + h * sh + c * 8) = pack8(f);
+}
+
+template <int D>
+void launch_slab_convert(const float* slab, void* out, const int64_t* st, int B, int S, int H, float scale, int Sq,
+                         int G, int causal, int coff, int chunk, int per_bh, hipStream_t stream) {
+  const int64_t nrows = (int64_t)B * H * S;
+  const int rows_per_block = 256 / (D / 8);
+  const int grid = (int)((nrows + rows_per_block - 1) / rows_per_block);
+  if (grid > 0)
+    hipLaunchKernelGGL(slab_convert_kernel<D>, dim3(grid), dim3(256), 0, stream, slab, (uint16_t*)out, st[0], st[1], st[2],
+                       B, S, H, scale, Sq, G, causal, coff, chunk, per_bh);
 }
 
 template <int D>
@@ -754,6 +832,21 @@ int chunk_override() {
   return g_chunk;
 }
 
+// dK/dV reduction across the items of a key block: 0 = f32 atomics into one accumulator, 1 = per-item
+// slabs written with plain stores and summed by the convert pass (NXD_FAB_DKV_SLAB, default 1).
+// Slabs take the 0.55 GB of dK/dV adds (S=8192, 32/8 heads) off the chip-wide f32 atomic rate the
+// kernel is bound by, for 0.55 GB of plain stores plus one read in the convert: 2.117 -> 2.008 ms
+// (32/8 heads), 1.072 -> 1.014 (TP=8 shape, B=4), 0.299 -> 0.275 (4/1, B=1); D=64 16/4 neutral
+// (profiles/r3_fab_slab_ab.jsonl).
+static int g_slab = -1;
+int slab_mode() {
+  if (g_slab < 0) {
+    const char* e = getenv("NXD_FAB_DKV_SLAB");
+    g_slab = e ? atoi(e) : 1;
+  }
+  return g_slab;
+}
+
 static int g_pipe = -1;
 int pipe_variant() {
   if (g_pipe < 0) {
@@ -781,13 +874,35 @@ void flash_attn_bwd_set_knob(int which, int value) {
   if (which == 1) fab::g_chunk = value;
   if (which == 3) fab::g_xcd = value;
   if (which == 4) fab::g_pipe = value;  // pipeline depths: 12 (default), 11, 21, 0
+  if (which == 5) fab::g_slab = value;  // dK/dV: 0 atomics, 1 per-item slabs
 }
 
-// fp32 workspace floats the backward needs: dq_acc + dk_acc + dv_acc + nlse + ndelta
-int64_t flash_attn_bwd_workspace(int B, int Sq, int Sk, int Hq, int Hkv, int D) {
+namespace fab {
+// work-item chunk length and items per (batch, kv head) of a launch (one definition for the
+// workspace sizing and the launch)
+void plan(int B, int Sq, int Sk, int Hq, int Hkv, int causal, int causal_offset, int* chunk, int64_t* per_bh) {
+  const int nkb = (Sk + kBlockK - 1) / kBlockK;
+  const int G = Hq / Hkv;
+  *chunk = chunk_override() > 0 ? chunk_override() : choose_chunk(nkb, Sq, G, causal, causal_offset, B * Hkv, num_cus());
+  int64_t n = 0;
+  for (int kb = 0; kb < nkb; ++kb) n += (kb_iters(kb, Sq, G, causal, causal_offset) + *chunk - 1) / *chunk;
+  *per_bh = n;
+}
+}  // namespace fab
+
+// fp32 workspace floats the backward needs: dq_acc + dk_acc + dv_acc + nlse + ndelta (+ the dK / dV
+// slabs in slab mode)
+int64_t flash_attn_bwd_workspace(int B, int Sq, int Sk, int Hq, int Hkv, int D, int causal, int causal_offset) {
   const int64_t Sq_pad = (Sq + fab::kBlockQ - 1) / fab::kBlockQ * fab::kBlockQ;
   const int64_t Sk_pad = (Sk + fab::kBlockK - 1) / fab::kBlockK * fab::kBlockK;
-  return (int64_t)B * Hq * Sq_pad * D + 2 * (int64_t)B * Hkv * Sk_pad * D + 2 * (int64_t)B * Hq * Sq;
+  int64_t n = (int64_t)B * Hq * Sq_pad * D + 2 * (int64_t)B * Hkv * Sk_pad * D + 2 * (int64_t)B * Hq * Sq;
+  if (fab::slab_mode() && Hkv > 0 && Hq % Hkv == 0) {
+    int chunk;
+    int64_t per_bh;
+    fab::plan(B, Sq, Sk, Hq, Hkv, causal, causal_offset, &chunk, &per_bh);
+    n += 2 * (int64_t)B * Hkv * per_bh * fab::kBlockK * D;
+  }
+  return n;
 }
 
 int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -807,8 +922,14 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   float* dv_acc = dk_acc + (int64_t)B * Hkv * Sk_pad * D;
   float* nlse = dv_acc + (int64_t)B * Hkv * Sk_pad * D;
   float* ndelta = nlse + (int64_t)B * Hq * Sq;
-  // one memset for the three accumulators (contiguous)
-  (void)hipMemsetAsync(ws, 0, (size_t)((int64_t)B * Hq * Sq_pad * D + 2 * (int64_t)B * Hkv * Sk_pad * D) * sizeof(float), stream);
+  int chunk;
+  int64_t per_bh;
+  plan(B, Sq, Sk, Hq, Hkv, causal, causal_offset, &chunk, &per_bh);
+  const bool slabs = slab_mode() != 0;
+  float* dk_slab = slabs ? ndelta + (int64_t)B * Hq * Sq : nullptr;
+  float* dv_slab = slabs ? dk_slab + (int64_t)B * Hkv * per_bh * kBlockK * D : nullptr;
+  // one memset for the accumulators (contiguous; the slabs are written whole by the kernel)
+  (void)hipMemsetAsync(ws, 0, (size_t)((int64_t)B * Hq * Sq_pad * D + (slabs ? 0 : 2 * (int64_t)B * Hkv * Sk_pad * D)) * sizeof(float), stream);
 
   const int64_t nrows = (int64_t)B * Hq * Sq;
   const int rows_per_block = 256 / (D / 8);
@@ -825,6 +946,7 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   BwdParams p;
   p.q = (const uint16_t*)q; p.k = (const uint16_t*)k; p.v = (const uint16_t*)v; p.dout = (const uint16_t*)dout;
   p.nlse = nlse; p.ndelta = ndelta; p.dq_acc = dq_acc; p.dk_acc = dk_acc; p.dv_acc = dv_acc;
+  p.dk_slab = dk_slab; p.dv_slab = dv_slab;
   p.q_sb = qs[0]; p.q_ss = qs[1]; p.q_sh = qs[2];
   p.k_sb = ks[0]; p.k_ss = ks[1]; p.k_sh = ks[2];
   p.v_sb = vs[0]; p.v_ss = vs[1]; p.v_sh = vs[2];
@@ -833,10 +955,8 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   p.scale_log2 = softmax_scale * 1.4426950408889634f;
   p.causal = causal; p.causal_offset = causal_offset;
 
-  p.chunk = chunk_override() > 0 ? chunk_override() : choose_chunk(nkb, Sq, G, causal, causal_offset, B * Hkv, num_cus());
-  int64_t items = 0;
-  for (int kb = 0; kb < nkb; ++kb) items += (kb_iters(kb, Sq, G, causal, causal_offset) + p.chunk - 1) / p.chunk;
-  items *= (int64_t)B * Hkv;
+  p.chunk = chunk;
+  const int64_t items = per_bh * B * Hkv;
   p.ablate = ablate_flags();
   p.xcd_map = xcd_map_mode();
   p.drop = drop;
@@ -861,12 +981,22 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   }
   if (D == 128) {
     launch_convert<128>(dq_acc, dq, dqs, B, Sq, (int)Sq_pad, Hq, softmax_scale, stream);
-    launch_convert<128>(dk_acc, dk, dks, B, Sk, (int)Sk_pad, Hkv, softmax_scale, stream);
-    launch_convert<128>(dv_acc, dv, dvs, B, Sk, (int)Sk_pad, Hkv, 1.f, stream);
+    if (slabs) {
+      launch_slab_convert<128>(dk_slab, dk, dks, B, Sk, Hkv, softmax_scale, Sq, G, causal, causal_offset, chunk, (int)per_bh, stream);
+      launch_slab_convert<128>(dv_slab, dv, dvs, B, Sk, Hkv, 1.f, Sq, G, causal, causal_offset, chunk, (int)per_bh, stream);
+    } else {
+      launch_convert<128>(dk_acc, dk, dks, B, Sk, (int)Sk_pad, Hkv, softmax_scale, stream);
+      launch_convert<128>(dv_acc, dv, dvs, B, Sk, (int)Sk_pad, Hkv, 1.f, stream);
+    }
   } else {
     launch_convert<64>(dq_acc, dq, dqs, B, Sq, (int)Sq_pad, Hq, softmax_scale, stream);
-    launch_convert<64>(dk_acc, dk, dks, B, Sk, (int)Sk_pad, Hkv, softmax_scale, stream);
-    launch_convert<64>(dv_acc, dv, dvs, B, Sk, (int)Sk_pad, Hkv, 1.f, stream);
+    if (slabs) {
+      launch_slab_convert<64>(dk_slab, dk, dks, B, Sk, Hkv, softmax_scale, Sq, G, causal, causal_offset, chunk, (int)per_bh, stream);
+      launch_slab_convert<64>(dv_slab, dv, dvs, B, Sk, Hkv, 1.f, Sq, G, causal, causal_offset, chunk, (int)per_bh, stream);
+    } else {
+      launch_convert<64>(dk_acc, dk, dks, B, Sk, (int)Sk_pad, Hkv, softmax_scale, stream);
+      launch_convert<64>(dv_acc, dv, dvs, B, Sk, (int)Sk_pad, Hkv, 1.f, stream);
+    }
   }
   return (int)hipGetLastError();
 }

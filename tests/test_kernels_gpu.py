@@ -110,6 +110,22 @@ def test_flash_bwd_chunked_items(D):
     _bwd_check(1, 4096, 4096, 4, 1, D, True)
 
 
+@pytest.mark.parametrize("slab", [0, 1])
+def test_flash_bwd_dkdv_slab_mode(slab):
+    # dK/dV of the work items of one key block summed through per-item slabs (plain stores +
+    # convert pass) instead of f32 atomics: same numerics, every shape class
+    ext = ops.ext()
+    ext.flash_attn_set_knob(5, slab)
+    try:
+        _bwd_check(1, 4096, 4096, 4, 1, 128, True)
+        _bwd_check(1, 2048, 2048, 8, 2, 64, True)
+        _bwd_check(2, 100, 300, 4, 2, 64, True)
+        _bwd_check(1, 300, 100, 2, 2, 128, False)
+        _bwd_check(2, 1024, 1024, 8, 2, 128, False)
+    finally:
+        ext.flash_attn_set_knob(5, -1)
+
+
 def test_flash_bwd_cross_lengths():
     _bwd_check(2, 100, 300, 4, 2, 64, True)  # bottom-right aligned causal, Sk not a block multiple
     _bwd_check(1, 300, 100, 2, 2, 128, False)
