@@ -126,7 +126,7 @@ def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_mode
     for ranks in pp_mesh:
         if rank in ranks:
             _PP_GLOBAL_RANKS = list(ranks)
-    if dist.get_backend() != "gloo":
+    if dist.get_backend() not in ("gloo", "fake"):   # ("fake": single-process rank emulation, tools/emulate_tp_rank.py)
         _WORLD_GLOO_GROUP = dist.new_group(list(range(world)), backend="gloo")
     else:
         _WORLD_GLOO_GROUP = dist.group.WORLD

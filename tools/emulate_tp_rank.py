@@ -1,0 +1,150 @@
+"""One tensor-parallel rank of the multi-GPU bench, emulated on ONE GPU without its peers.
+
+torch.distributed runs on the in-process "fake" backend with world size = TP and this process as
+rank 0, so the model is built and stepped exactly as `bench.py --gpus TP` builds it on a node:
+the real TP shards (32/TP q heads, 8/TP kv heads, FFN and vocabulary split), sequence-parallel
+activations (RMSNorm, residual adds and embeddings on S/TP rows, the chunked all-gather -> GEMM
+and GEMM -> reduce-scatter pipelines of parallel_layers/sp.py), the vocabulary-parallel embedding
+and cross-entropy, fp32-master AdamW with the global grad-norm clip.  Only the links are missing:
+each collective is replaced by the local HBM work it does on the receiving side (an all-gather
+writes the whole output buffer -- filled with copies of the local shard so values stay finite --
+a reduce-scatter writes its shard, an all-reduce leaves the tensor as is).
+
+The step time is therefore the per-rank compute floor of the N-GPU bench; tokens/s = global batch
+x sequence / step time is the whole-node throughput at perfect communication overlap.  It is not
+a throughput claim (the driver's node run is).
+
+    python tools/emulate_tp_rank.py --tp 8 --steps 3 --warmup 1
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from neuronx_distributed_llama3_2_amd.parallel import comm  # noqa: E402
+
+
+class _Done:
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+def _emulate_collectives():
+    """Receiving-side HBM work of each collective, no links (see module docstring)."""
+
+    def all_gather_into_tensor(out, inp, group=None, async_op=False):
+        ws = dist.get_world_size(group=group)
+        inp = inp.contiguous()
+        out.view((ws,) + tuple(inp.shape)).copy_(inp.unsqueeze(0).expand((ws,) + tuple(inp.shape)))
+        return _Done() if async_op else None
+
+    def reduce_scatter_tensor(out, inp, group=None, async_op=False, op=dist.ReduceOp.SUM):
+        ws = dist.get_world_size(group=group)
+        out.copy_(inp.contiguous().view((ws,) + tuple(out.shape))[0])
+        return _Done() if async_op else None
+
+    def all_reduce(t, group=None, async_op=False, op=dist.ReduceOp.SUM):
+        return _Done() if async_op else None
+
+    def all_reduce_coalesced(tensors, group=None):
+        return None
+
+    comm.all_gather_into_tensor = all_gather_into_tensor
+    comm.reduce_scatter_tensor = reduce_scatter_tensor
+    comm.all_reduce = all_reduce
+    comm.all_reduce_coalesced = all_reduce_coalesced
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tp", type=int, default=8)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq", type=int, default=8192)
+    ap.add_argument("--layers", type=int, default=None, help="override #layers (default: the full model)")
+    ap.add_argument("--mbs", type=int, default=None, help="default: bench.py's MBS_BY_TP")
+    ap.add_argument("--gbs", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--no-sp", action="store_true")
+    ap.add_argument("--cpu", action="store_true", help="plumbing check on the CPU (tiny models)")
+    ap.add_argument("--hidden", type=int, default=None, help="(CPU plumbing) override hidden size")
+    a = ap.parse_args()
+
+    from torch.testing._internal.distributed.fake_pg import FakeStore
+
+    import bench
+    from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
+    from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW
+    from neuronx_distributed_llama3_2_amd.parallel.grad_buffer import find_shared_params
+    from neuronx_distributed_llama3_2_amd.parallel_layers import parallel_state as ps
+    from neuronx_distributed_llama3_2_amd.parallel_layers.random import model_parallel_manual_seed
+
+    use_cuda = torch.cuda.is_available() and not a.cpu
+    dev = torch.device("cuda", 0) if use_cuda else torch.device("cpu")
+    if use_cuda:
+        torch.cuda.set_device(0)
+    dist.init_process_group("fake", rank=0, world_size=a.tp, store=FakeStore())
+    _emulate_collectives()
+    ps.initialize_model_parallel(tensor_model_parallel_size=a.tp)
+    model_parallel_manual_seed(1234)
+    over = dict(sequence_parallel_enabled=(a.tp > 1 and not a.no_sp), max_position_embeddings=max(8192, a.seq))
+    if a.layers is not None:
+        over["num_hidden_layers"] = a.layers
+    if a.hidden is not None:
+        over.update(hidden_size=a.hidden, intermediate_size=4 * a.hidden, vocab_size=1024 * a.tp)
+    cfg = llama_config(a.model, **over)
+    mbs = a.mbs if a.mbs is not None else bench.MBS_BY_TP.get(a.tp, 1)
+    accum = a.gbs // mbs
+    model = LlamaForCausalLM(cfg, dtype=torch.bfloat16, device=dev)
+    model.train()
+    decay = [p for n, p in model.named_parameters() if p.dim() > 1]
+    no_decay = [p for n, p in model.named_parameters() if p.dim() <= 1]
+    opt = FlatMixedPrecisionAdamW([{"params": decay, "weight_decay": 0.01}, {"params": no_decay, "weight_decay": 0.0}],
+                                  lr=1e-5, betas=(0.9, 0.95), eps=1e-8, zero1=False, grad_clipping=True,
+                                  max_grad_norm=1.0, shared_param_ids=find_shared_params(model))
+    g = torch.Generator(device="cpu").manual_seed(4321)
+    n_mb = (a.warmup + a.steps) * accum
+    batches = torch.randint(0, cfg.vocab_size, (n_mb, mbs, a.seq), generator=g).to(dev)
+    cursor = [0]
+
+    def step():
+        for i in range(accum):
+            opt.set_grad_sync(i == accum - 1)
+            ids = batches[cursor[0]]
+            cursor[0] += 1
+            out = model(ids, labels=ids)
+            (out.loss / accum).backward()
+        opt.step()
+        opt.zero_grad()
+
+    for _ in range(a.warmup):
+        step()
+    if use_cuda:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    if use_cuda:
+        torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / a.steps
+    rec = {"tool": "emulate_tp_rank", "tp": a.tp, "sp": over["sequence_parallel_enabled"], "model": a.model,
+           "layers": cfg.num_hidden_layers, "seq": a.seq, "mbs": mbs, "gbs": a.gbs, "grad_accum": accum,
+           "ms_per_step": round(1000 * el, 2), "ms_per_microbatch": round(1000 * el / accum, 2),
+           "node_tokens_per_s_comm_free": round(a.gbs * a.seq / el, 1),
+           "params_per_rank": sum(p.numel() for p in model.parameters()),
+           "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if use_cuda else 0.0}
+    print(json.dumps(rec), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
