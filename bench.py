@@ -1,7 +1,7 @@
 """Headline benchmark: Llama-3-8B bf16 pre-training throughput (tokens/s, whole job) on N MI355X.
 
 Config (BASELINE.json): Llama-3-8B architecture (random init, synthetic token data), sequence
-length 8192, micro-batch 1, tensor parallel TP = N (<= 8) with sequence parallelism, flash
+length 8192, micro-batch per TP degree (MBS_BY_TP), tensor parallel TP = N (<= 8) with sequence parallelism, flash
 attention, fp32 master weights + fused AdamW (ZeRO-1 when DP > 1), gradient accumulation up to the
 global batch.  `--parallelism dp` instead runs TP=1 x DP=N (weak scaling).  `--pp P` runs the
 BASELINE's pipeline config: TP = N / P x PP = P through NxDPPModel's 1F1B schedule (P2P over RCCL
@@ -34,11 +34,16 @@ sys.path.insert(0, ROOT)
 os.environ.setdefault("NXD_LOG_STREAM", "stderr")
 
 # Micro-batch per TP degree: TP shrinks every per-rank GEMM and the attention head count, so the
-# TP=4/8 ranks process several sequences per micro-batch to keep MFMA tiles and the attention grid
-# full (global batch unchanged).  Per-GPU compute-only throughput at TP-8 shapes, mbs 1 / 2 / 4 / 8:
-# 367k / 391k / 415k / 414k tokens/s; TP-4 219k / 229k / 233k / 231k; TP-2 120k / 124k / 122k;
-# TP-1 63k / 63k (profiles/r2_mbs_sweep.jsonl, 8 layers).  TP-1 keeps 1: +1 % is not worth 10 GiB.
-MBS_BY_TP = {1: 1, 2: 2, 4: 4, 8: 4}
+# TP>1 ranks process several sequences per micro-batch to keep MFMA tiles and the attention grid
+# full (global batch unchanged; 288 GB per GPU has room for it).  Full-model step of one emulated
+# TP rank (tools/emulate_tp_rank.py, real TP + SP code path, no links; profiles/r3_emulate_mbs.jsonl):
+# TP-8 mbs 4 / 8: 412 / 387 ms (52 / 85 GiB); TP-4 mbs 4 / 8: 733 / 696 ms (88 / 136 GiB); TP-2 mbs
+# 2 / 4: 1418 / 1373 ms (117 / 159 GiB).  The SP collectives keep their total bytes and chunk count.
+# TP-1 mbs 1 / 2 on one box, alternating: 3071 / 3035 ms and 3069 / 3011 ms per step, peak 187 / 225 GiB
+# allocated, 190 / 228 GiB reserved of 268 GiB (profiles/r3_bench_mbs_tp1_ab.txt).
+MBS_BY_TP = {1: 2, 2: 4, 4: 8, 8: 8}
+# --pp: smaller micro-batches, the 1F1B bubble is (P-1)/(M+P-1) for M micro-batches
+MBS_BY_TP_PP = {1: 1, 2: 2, 4: 4, 8: 4}
 
 BASELINE_TOKENS_PER_S = None  # the reference publishes no Llama-3-8B throughput
 
@@ -194,7 +199,7 @@ def main(a):
         over["selective_checkpoint_enabled"] = True
     cfg = llama_config(a.model, **over)
     if a.mbs is None:
-        a.mbs = max(1, min(MBS_BY_TP.get(tp, 1), a.gbs // dp))
+        a.mbs = max(1, min((MBS_BY_TP_PP if a.pp > 1 else MBS_BY_TP).get(tp, 1), a.gbs // dp))
     if a.gbs % (a.mbs * dp):
         raise SystemExit(f"bench: global batch {a.gbs} not divisible by micro-batch {a.mbs} x DP {dp}")
     accum = a.gbs // (a.mbs * dp)
@@ -294,6 +299,7 @@ def main(a):
             "model_params": nparams,
             "mfu": round(mfu(value, fpt, world), 4),   # vs 2.5 PFLOP/s dense bf16 per GPU
             "peak_mem_gib": round(mem, 1),
+            "peak_reserved_gib": round(torch.cuda.max_memory_reserved(dev) / 2**30, 1) if use_cuda else 0.0,
         }
         print(json.dumps(rec), flush=True)
     dist.barrier()
