@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <map>
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -48,10 +49,11 @@ struct Problem {
   int64_t rowsA, colsA, lda, rowsB, colsB, ldb, ldc, ldd;
   int ta, tc;               // input / output hipDataType
   int beta_nonzero;
+  bool no_sk = false;
   std::string key() const {
     std::ostringstream s;
     s << opA << ' ' << opB << ' ' << m << ' ' << n << ' ' << k << ' ' << lda << ' ' << ldb << ' ' << ldc << ' ' << ldd
-      << ' ' << ta << ' ' << tc << ' ' << beta_nonzero;
+      << ' ' << ta << ' ' << tc << ' ' << beta_nonzero << (no_sk ? " nosk" : "");
     return s.str();
   }
 };
@@ -81,15 +83,17 @@ class Tuner {
     return handles_[dev];
   }
 
-  void* workspace(size_t bytes) {
+  // one workspace per (device, stream): GEMMs on concurrent streams (the two sequence-parallel
+  // halves of parallel_layers/stream_split.py) must not share split-K / stream-K partials
+  void* workspace(size_t bytes, hipStream_t stream) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> g(mu_);
-    if ((int)ws_.size() <= dev) ws_.resize(dev + 1);
-    if (ws_[dev].numel() < (int64_t)bytes) {
-      ws_[dev] = at::empty({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
+    at::Tensor& w = ws_[std::make_pair(dev, (uintptr_t)stream)];
+    if (w.numel() < (int64_t)bytes) {
+      w = at::empty({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
     }
-    return ws_[dev].data_ptr();
+    return w.data_ptr();
   }
 
   size_t max_ws() const { return ws_limit_; }
@@ -185,7 +189,7 @@ class Tuner {
 
   std::mutex mu_;
   std::vector<hipblasLtHandle_t> handles_;
-  std::vector<at::Tensor> ws_;
+  std::map<std::pair<int, uintptr_t>, at::Tensor> ws_;
   std::unordered_map<std::string, Choice> cache_;
   std::string file_, table_, log_;
   std::unordered_set<std::string> logged_;
@@ -194,6 +198,28 @@ class Tuner {
   int mode_ = 1, candidates_ = 24;
   size_t ws_limit_ = 128u << 20;
 };
+
+// Overlap-safe selection (NXD_GEMM_NO_STREAMK / gemm_set_no_streamk): skip hipBLASLt's stream-K
+// solutions ("_SK<n>" in the kernel name).  A stream-K GEMM runs one persistent workgroup per CU
+// whose partial tiles are fixed up by the others; when a concurrent kernel (an RCCL channel, one
+// workgroup) holds a CU, the fix-ups wait for the displaced workgroup and the GEMM takes ~1.8x as
+// long (TP=8 gate_up / o_proj shapes with 4 side workgroups, profiles/r3_cu_interference.jsonl),
+// where a data-parallel tile kernel only loses its tail.  Multi-rank training (collectives
+// overlapping GEMMs) turns it on; -1 = not set (env, else off).
+static int g_no_streamk = -1;
+static bool no_streamk() {
+  if (g_no_streamk < 0) {
+    const char* e = std::getenv("NXD_GEMM_NO_STREAMK");
+    g_no_streamk = (e && std::atoi(e) > 0) ? 1 : 0;
+  }
+  return g_no_streamk == 1;
+}
+static bool is_streamk(hipblasLtHandle_t h, hipblasLtMatmulAlgo_t algo) {
+  const std::string n = hipblaslt_ext::getKernelNameFromAlgo(h, algo);
+  for (size_t i = n.find("_SK"); i != std::string::npos; i = n.find("_SK", i + 1))
+    if (i + 3 < n.size() && n[i + 3] >= '1' && n[i + 3] <= '9') return true;
+  return false;
+}
 
 static hipDataType dt(const at::Tensor& t) {
   switch (t.scalar_type()) {
@@ -299,6 +325,7 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
   p.ta = dt(a);
   p.tc = dt(d);
   p.beta_nonzero = beta_d != 0.0;
+  p.no_sk = no_streamk();
   const float alpha = (float)alpha_d, beta = (float)beta_d;
   auto& T = Tuner::get();
   hipblasLtHandle_t h = T.handle();
@@ -326,15 +353,16 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
       known = false;  // stale entry (different library build): tune again
     }
   }
-  if (!known && T.mode() >= 2 && !capturing(s)) {
+  if (!known && (T.mode() >= 2 || p.no_sk) && !capturing(s)) {
     // exhaustive: every library solution for this (ops, dtypes), filtered by support, timed once,
-    // the five fastest re-timed
+    // the five fastest re-timed (overlap-safe mode always takes this path: for many gfx950 shapes
+    // the whole heuristic list is stream-K variants)
     std::vector<hipblasLtMatmulHeuristicResult_t> all;
     LT_CHECK(hipblaslt_ext::getAllAlgos(h, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, (hipblasOperation_t)p.opA,
                                         (hipblasOperation_t)p.opB, (hipDataType)p.ta, (hipDataType)p.ta,
                                         (hipDataType)p.tc, (hipDataType)p.tc, HIPBLAS_COMPUTE_32F, all));
     const size_t wsmax = T.max_ws();
-    void* wsp = T.workspace(wsmax);
+    void* wsp = T.workspace(wsmax, s);
     at::Tensor scratch;
     void* Dp = d.data_ptr();
     if (p.beta_nonzero) {
@@ -348,13 +376,25 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
       size_t wsz = 0;
       if (hipblaslt_ext::matmulIsAlgoSupported(h, ds.op, &alpha, ds.A, ds.B, &beta, ds.C, ds.D, all[i].algo, wsz) !=
               HIPBLAS_STATUS_SUCCESS ||
-          wsz > wsmax)
+          wsz > wsmax || (p.no_sk && is_streamk(h, all[i].algo)))
         continue;
       ++tried;
       wss[i] = wsz;
       float ms = time_algo(h, ds, all[i].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(), c.data_ptr(), Dp, wsp, wsmax,
                            s, 1);
       if (ms > 0.f) timed.emplace_back(ms, (int)i);
+    }
+    if (timed.empty() && p.no_sk) {  // no data-parallel solution at all: allow stream-K
+      for (size_t i = 0; i < all.size() && (int)timed.size() < T.max_algos(); ++i) {
+        size_t wsz = 0;
+        if (hipblaslt_ext::matmulIsAlgoSupported(h, ds.op, &alpha, ds.A, ds.B, &beta, ds.C, ds.D, all[i].algo, wsz) !=
+                HIPBLAS_STATUS_SUCCESS || wsz > wsmax)
+          continue;
+        wss[i] = wsz;
+        float ms = time_algo(h, ds, all[i].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(), c.data_ptr(), Dp, wsp,
+                             wsmax, s, 1);
+        if (ms > 0.f) timed.emplace_back(ms, (int)i);
+      }
     }
     TORCH_CHECK(!timed.empty(), "gemm: no supported hipBLASLt solution for ", key);
     std::sort(timed.begin(), timed.end());
@@ -378,6 +418,9 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
     ch.resolved = true;
     known = true;
     T.store(key, ch, true);
+    if (std::getenv("NXD_GEMM_LOG_CHOICE"))
+      std::fprintf(stderr, "[nxd gemm] %s -> %s %.4f ms (exhaustive, %zu timed)\n", key.c_str(),
+                   hipblaslt_ext::getKernelNameFromAlgo(h, ch.algo).c_str(), best_ms, timed.size());
   }
   if (!known || !ch.resolved) {
     hipblasLtMatmulPreference_t pref;
@@ -386,18 +429,30 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
     LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsmax,
                                                   sizeof(wsmax)));
     const bool tune = !known && T.mode() >= 1 && !capturing(s);
-    const int want = (tune || known) ? T.candidates() : 1;
+    // (overlap-safe: a wider heuristic list, the top of which can be all stream-K variants)
+    const int want = p.no_sk ? std::max(4 * T.candidates(), 96) : ((tune || known) ? T.candidates() : 1);
     std::vector<hipblasLtMatmulHeuristicResult_t> res(want);
     int got = 0;
     LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, ds.op, ds.A, ds.B, ds.C, ds.D, pref, want, res.data(), &got));
     hipblasLtMatmulPreferenceDestroy(pref);
     TORCH_CHECK(got > 0, "gemm: no hipBLASLt solution for ", key);
+    // overlap-safe: candidates other than stream-K (all of them if every candidate is stream-K)
+    std::vector<char> skip(got, 0);
+    if (p.no_sk) {
+      int left = 0;   // keep the first candidates() non-stream-K entries
+      for (int i = 0; i < got; ++i) {
+        skip[i] = is_streamk(h, res[i].algo) || left >= T.candidates();
+        left += !skip[i];
+      }
+      if (left == 0) std::fill(skip.begin(), skip.end(), 0);
+    }
     int best = 0;
+    while (best + 1 < got && skip[best]) ++best;
     float best_ms = ch.ms;
     if (known) {
-      best = (ch.pos < got && res[ch.pos].state == HIPBLAS_STATUS_SUCCESS) ? ch.pos : 0;
+      if (ch.pos < got && res[ch.pos].state == HIPBLAS_STATUS_SUCCESS && !skip[ch.pos]) best = ch.pos;
     } else if (tune && got > 1) {
-      void* ws = T.workspace(wsmax);
+      void* ws = T.workspace(wsmax, s);
       at::Tensor scratch;
       void* Dp = d.data_ptr();
       if (p.beta_nonzero) {  // never accumulate repeatedly into the real output
@@ -408,7 +463,7 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
       const int reps = flops > 1e12 ? 3 : (flops > 1e10 ? 8 : 20);
       best = -1;
       for (int i = 0; i < got; ++i) {
-        if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > wsmax) continue;
+        if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > wsmax || skip[i]) continue;
         float ms = time_algo(h, ds, res[i].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(), c.data_ptr(), Dp, ws,
                              wsmax, s, reps);
         if (ms > 0.f && (best < 0 || ms < best_ms)) {
@@ -424,13 +479,19 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
     ch.pos = best;
     ch.resolved = true;
     T.store(key, ch, tune && got > 1);
+    if (std::getenv("NXD_GEMM_LOG_CHOICE"))  // which kernel each new problem runs (stderr)
+      std::fprintf(stderr, "[nxd gemm] %s -> %s %.4f ms (pos %d of %d)\n", key.c_str(),
+                   hipblaslt_ext::getKernelNameFromAlgo(h, ch.algo).c_str(), best_ms, best, got);
   }
-  void* ws = ch.ws ? T.workspace(std::max<size_t>(ch.ws, T.max_ws())) : nullptr;
+  void* ws = ch.ws ? T.workspace(std::max<size_t>(ch.ws, T.max_ws()), s) : nullptr;
   LT_CHECK(hipblasLtMatmul(h, ds.op, &alpha, b.data_ptr(), ds.A, a.data_ptr(), ds.B, &beta, c.data_ptr(), ds.C,
                            d.data_ptr(), ds.D, &ch.algo, ws, ch.ws ? std::max<size_t>(ch.ws, T.max_ws()) : 0, s));
 }
 
 std::vector<std::pair<std::string, float>> gemm_tuned_entries() { return Tuner::get().entries(); }
+
+void gemm_set_no_streamk(int v) { g_no_streamk = v < 0 ? -1 : (v > 0 ? 1 : 0); }
+bool gemm_no_streamk() { return no_streamk(); }
 
 }  // namespace nxd_gemm
 
@@ -439,4 +500,6 @@ void register_gemm(pybind11::module& m) {
         pybind11::arg("b"), pybind11::arg("d"), pybind11::arg("c") = pybind11::none(), pybind11::arg("alpha") = 1.0,
         pybind11::arg("beta") = 0.0);
   m.def("gemm_tuned_entries", &nxd_gemm::gemm_tuned_entries);
+  m.def("gemm_set_no_streamk", &nxd_gemm::gemm_set_no_streamk, "1: skip stream-K solutions, 0: allow, -1: env");
+  m.def("gemm_no_streamk", &nxd_gemm::gemm_no_streamk);
 }

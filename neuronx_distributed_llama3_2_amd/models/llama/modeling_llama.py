@@ -34,7 +34,9 @@ from ...parallel_layers.layer_norm import RMSNorm
 from ...parallel_layers.layers import ColumnParallelLinear, ParallelEmbedding, RowParallelLinear
 from ...parallel_layers.loss_functions import parallel_cross_entropy
 from ...parallel_layers.mappings import gather_from_sequence_parallel_region, scatter_to_sequence_parallel_region
-from ...parallel_layers.parallel_state import get_tensor_model_parallel_size
+from ...parallel_layers import stream_split
+from ...parallel_layers.parallel_state import (get_data_parallel_size, get_pipeline_model_parallel_size,
+                                                      get_tensor_model_parallel_size)
 from ...parallel_layers.utils import divide
 
 
@@ -170,6 +172,35 @@ class LlamaDecoderLayer(nn.Module):
         normed, residual = self.post_attention_layernorm(attn, residual)
         return self.mlp(normed), residual
 
+    def forward_stages(self, hidden_states, residual=None):
+        """`forward` as a generator that yields after every op that issues a sequence-parallel
+        collective (qkv all-gather, o_proj reduce-scatter, gate_up all-gather, down reduce-scatter),
+        for the two-stream interleaving of parallel_layers/stream_split.py."""
+        if residual is None:
+            normed = self.input_layernorm(hidden_states)
+            residual = hidden_states
+        else:
+            normed, residual = self.input_layernorm(hidden_states, residual)
+        att = self.self_attn
+        qkv = att.qkv_proj.forward_fused(normed)
+        yield
+        cos_t, sin_t = att.rope_cache.tables(qkv.device)
+        o = ops.rope_attention(qkv, cos_t, sin_t, att.num_heads_local, att.num_kv_heads_local, att.head_dim,
+                               causal=True)
+        attn = att.o_proj(o)
+        yield
+        normed, residual = self.post_attention_layernorm(attn, residual)
+        mlp = self.mlp
+        gu = mlp.gate_up_proj(normed)
+        yield
+        if mlp.selective_checkpoint and self.training:
+            h = checkpoint(ops.swiglu, gu, True, use_reentrant=False)
+        else:
+            h = ops.swiglu(gu, token_major=True)
+        out = mlp.down_proj(h)
+        yield
+        return out, residual
+
 
 class LlamaModel(nn.Module):
     def __init__(self, config, dtype=torch.bfloat16, device=None):
@@ -220,20 +251,59 @@ class LlamaForCausalLM(nn.Module):
 
     def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                 labels: Optional[torch.Tensor] = None, position_ids=None, **unused) -> CausalLMOutput:
+        if self._interleave(input_ids, labels):
+            return self._forward_interleaved(input_ids, attention_mask, labels)
         hidden = self.model(input_ids)
         logits = self.lm_head(hidden)  # [S, B, V/tp]
         loss = None
         if labels is not None:
-            # predict token s+1 at position s: shift labels, ignore the last position
-            lab = labels.t()  # [S, B]
-            nxt = lab[1:]
-            if attention_mask is not None:
-                nxt = torch.where(attention_mask.t()[1:] > 0, nxt, torch.full_like(nxt, -100))
-            shifted = torch.cat([nxt, torch.full_like(lab[:1], -100)], dim=0)
-            per_tok = parallel_cross_entropy(logits, shifted, inplace_backward=True)
-            n = (shifted != -100).sum().clamp(min=1)
-            loss = per_tok.sum() / n
+            tok_sum, n = self._loss_terms(logits, labels, attention_mask)
+            loss = tok_sum / n
         return CausalLMOutput(loss=loss, logits=logits)
+
+    @staticmethod
+    def _loss_terms(logits, labels, attention_mask):
+        """(sum of per-token losses, token count) -- predict token s+1 at position s."""
+        lab = labels.t()  # [S, B]
+        nxt = lab[1:]
+        if attention_mask is not None:
+            nxt = torch.where(attention_mask.t()[1:] > 0, nxt, torch.full_like(nxt, -100))
+        shifted = torch.cat([nxt, torch.full_like(lab[:1], -100)], dim=0)
+        per_tok = parallel_cross_entropy(logits, shifted, inplace_backward=True)
+        return per_tok.sum(), (shifted != -100).sum().clamp(min=1)
+
+    def _interleave(self, input_ids, labels) -> bool:
+        m = self.model
+        if isinstance(input_ids, torch.fx.Proxy) or torch.fx._symbolic_trace.is_fx_tracing():
+            return False   # pipeline partitioning traces the one-pass forward
+        return (stream_split.enabled() and self.training and torch.is_grad_enabled() and labels is not None
+                and get_pipeline_model_parallel_size() == 1
+                and m.sequence_parallel_enabled and m.activation_checkpoint != "full"
+                and input_ids.dim() == 2 and input_ids.shape[0] % 2 == 0 and get_data_parallel_size() == 1)
+
+    def _half(self, ids, labels, attention_mask):
+        m = self.model
+        hidden = m.embed_tokens(ids.t().contiguous())
+        residual = None
+        for layer in m.layers:
+            hidden, residual = yield from layer.forward_stages(hidden, residual)
+        hidden = m.norm(hidden, residual)[0]
+        logits = self.lm_head(hidden)
+        yield
+        return self._loss_terms(logits, labels, attention_mask)
+
+    def _forward_interleaved(self, input_ids, attention_mask, labels) -> CausalLMOutput:
+        """Training forward of TP + SP as two half micro-batches on two streams, their collectives
+        interleaved (parallel_layers/stream_split.py); same loss as the one-pass forward."""
+        h = input_ids.shape[0] // 2
+        am = (attention_mask[:h], attention_mask[h:]) if attention_mask is not None else (None, None)
+        gens = [self._half(input_ids[:h], labels[:h], am[0]), self._half(input_ids[h:], labels[h:], am[1])]
+        (s0, n0), (s1, n1) = stream_split.run_interleaved(gens, input_ids.device)
+        if input_ids.is_cuda:
+            for t in (s0, n0, s1, n1):   # made on the halves' streams, read on this one
+                t.record_stream(torch.cuda.current_stream())
+        loss = (s0 + s1) / (n0 + n1)
+        return CausalLMOutput(loss=loss, logits=None)
 
 
 def llama_config(name: str = "llama3-8b", **overrides):

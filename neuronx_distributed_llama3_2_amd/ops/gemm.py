@@ -16,6 +16,18 @@ from ._ext import ext, use_native
 _ENABLED = os.environ.get("NXD_TUNED_GEMM", "1") == "1"
 
 
+def set_overlap_safe(enabled: bool) -> None:
+    """Select GEMM solutions without stream-K (csrc/gemm.cpp `no_streamk`): a persistent stream-K
+    GEMM stalls while a concurrent collective holds one of its CUs.  Multi-rank training turns it
+    on (parallel_state.initialize_model_parallel) unless NXD_GEMM_NO_STREAMK is set."""
+    if "NXD_GEMM_NO_STREAMK" in os.environ or not torch.cuda.is_available():
+        return
+    try:
+        ext().gemm_set_no_streamk(1 if enabled else 0)
+    except Exception:  # extension not built (CPU-only environments)
+        pass
+
+
 def _native(*t: torch.Tensor) -> bool:
     return _ENABLED and use_native(*t) and all(x.dtype in (torch.bfloat16, torch.float16) for x in t)
 
@@ -106,7 +118,9 @@ def _use_wgrad_kernel(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor, has
 
 
 def _wgrad_scratch(n: int, dtype, device, tag: str = "") -> torch.Tensor:
-    key = (dtype, str(device), tag)
+    # one buffer per stream: the two halves of parallel_layers/stream_split.py transpose concurrently
+    sid = torch.cuda.current_stream(device).stream_id if torch.device(device).type == "cuda" else 0
+    key = (dtype, str(device), tag, sid)
     t = _scratch.get(key)
     if t is None or t.numel() < n:
         t = _scratch[key] = torch.empty(n, dtype=dtype, device=device)
@@ -192,12 +206,20 @@ def transpose(src: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
 def _kmajor(weight: torch.Tensor) -> torch.Tensor:
     key = (_weight_epoch[0], weight._version, weight.data_ptr())
     wt = getattr(weight, "_nxd_wt", None)
+    cur = torch.cuda.current_stream(weight.device)
     if wt is None or getattr(weight, "_nxd_wt_key", None) != key:
         if wt is None or wt.shape != (weight.shape[1], weight.shape[0]):
             wt = torch.empty((weight.shape[1], weight.shape[0]), dtype=weight.dtype, device=weight.device)
         transpose(weight.detach(), out=wt)
         weight._nxd_wt = wt
         weight._nxd_wt_key = key
+        weight._nxd_wt_ev = torch.cuda.Event()
+        weight._nxd_wt_ev.record(cur)
+        weight._nxd_wt_stream = cur.stream_id
+    elif getattr(weight, "_nxd_wt_stream", cur.stream_id) != cur.stream_id:
+        # written on another stream (the other half of stream_split): wait for the transpose
+        cur.wait_event(weight._nxd_wt_ev)
+        wt.record_stream(cur)
     return wt
 
 

@@ -70,7 +70,13 @@ class RMSNormFunc(torch.autograd.Function):
             dw = torch.empty(w.numel(), dtype=torch.float32, device=w.device)
             accumulate = False
         dres = dh_extra.contiguous() if (ctx.has_res and dh_extra is not None) else None
+        if accumulate:
+            from ..parallel_layers import stream_split   # (lazy: parallel_layers imports ops)
+
+            stream_split.accumulate_begin(w)
         ext().rmsnorm_bwd(dy, h, w, rstd, dres, dx, dw.view(-1), accumulate)
+        if accumulate:
+            stream_split.accumulate_end(w)
         gw = _weight_grad(w, dw)
         if ctx.has_res:
             # h = x + residual: both inputs get the same gradient

@@ -28,6 +28,7 @@ from .. import ops
 from ..parallel import comm
 from ..parallel.grad_buffer import KIND_DUP, KIND_DUP_SP, KIND_SHARDED, FlatBuffer, find_shared_params, param_kind
 from ..parallel_layers import parallel_state as ps
+from ..parallel_layers import stream_split
 
 
 class _BufferState:
@@ -153,6 +154,7 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
             b.buf.set_sync(enabled)
 
     def zero_grad(self, set_to_none: bool = True) -> None:
+        stream_split.join()
         for b in self.buffers:
             b.buf.zero_grad()
 
@@ -213,6 +215,7 @@ class FlatMixedPrecisionAdamW(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        stream_split.join()   # the two-stream SP halves' last weight gradients
         self._sync_grads()
         coef = None
         if self.grad_clipping:

@@ -34,6 +34,7 @@ from torch.nn.parameter import Parameter
 from .. import ops
 from ..ops import gemm as _gemm
 from ..ops.activations import attached_token_major
+from . import stream_split
 from . import sp
 from .mappings import (
     _gather_along_first_dim,
@@ -94,7 +95,9 @@ def _accumulate_wgrad(weight: torch.Tensor, go2: torch.Tensor, x2, go_t: torch.T
     mg = getattr(weight, "main_grad", None)
     if mg is None:
         return go2.t().matmul(x2 if x2 is not None else x_t.t())
+    stream_split.accumulate_begin(weight)
     _gemm.wgrad_accumulate_(mg, go2, x2, go_t=go_t, x_t=x_t)
+    stream_split.accumulate_end(weight)
     _notify(weight)
     return None
 
@@ -114,7 +117,9 @@ def _bias_grad(bias, go2):
     g = go2.sum(0)
     mg = getattr(bias, "main_grad", None)
     if mg is not None:
+        stream_split.accumulate_begin(bias)
         mg.add_(g.float())
+        stream_split.accumulate_end(bias)
         _notify(bias)
         return None
     return g.to(bias.dtype)

@@ -115,9 +115,11 @@ def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_mode
     if ep > 1:
         logger.info("> initializing expert model parallel with size %d (expert data parallel %d)", ep, edp)
     _TP_MESH, _DP_MESH, _PP_MESH, _EP_MESH, _EDP_MESH = tp_mesh, dp_mesh, pp_mesh, ep_mesh, edp_mesh
+    from ..ops.gemm import set_overlap_safe
     from ..parallel.rccl_env import log_comm_config
 
     log_comm_config()
+    set_overlap_safe(world > 1)   # collectives will overlap GEMMs: no stream-K GEMM solutions
     _TP_GROUP = _assign(tp_mesh, rank, high_priority=True)
     _DP_GROUP = _assign(dp_mesh, rank)
     _PP_GROUP = _assign(pp_mesh, rank)

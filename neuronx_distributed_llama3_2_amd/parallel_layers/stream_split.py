@@ -1,0 +1,119 @@
+"""Two-stream micro-batch interleaving for tensor + sequence parallel training.
+
+Why: at TP = 8 the SP collectives of one Llama-3-8B layer move as many bytes per token as the
+layer's GEMMs take time (8 all-gathers / reduce-scatters of hidden x 2 B per token and layer), and
+inside ONE sequence the chunked GEMM <-> collective pipelines of `sp.py` can only hide a
+collective behind the GEMM that consumes or produces it -- attention, norms and SwiGLU leave the
+links idle and the next collective waits for them.  An emulated TP=8 rank with a 400 GB/s link
+model (tools/emulate_tp_rank.py --link-gbps 400) spends 603 ms per step against 388 ms of compute
+and 305 ms of link time.
+
+How: the micro-batch is split into two halves whose forward passes are issued alternately, one
+collective-bearing op at a time, each half on its own HIP stream.  The single RCCL stream then
+carries A's all-gather, B's all-gather, A's reduce-scatter, ... while the compute streams run the
+other half's attention / MLP.  Autograd runs every backward op on its forward op's stream and
+orders the ready ops by creation, so the backward interleaves the same way with no extra code.
+
+Shared state the two streams write is serialised here:
+* fp32 `main_grad` accumulation (weight-gradient GEMMs with beta = 1, RMSNorm dw): a per-parameter
+  event orders the two halves' read-modify-writes (`accumulate_begin` / `accumulate_end`);
+* the lazily built K-major weight copies and the wgrad transposes' scratch (ops/gemm.py) and the
+  hipBLASLt workspace (csrc/gemm.cpp) are per stream or event-ordered;
+* `join()` makes the caller's stream wait for both halves (the optimizer step calls it).
+
+Active only while training with TP > 1, sequence parallelism, DP = 1 (the backward-overlapped DP
+bucket reduction counts one gradient report per parameter) and no full activation checkpointing;
+NXD_SP_STREAMS=1 turns it off, =2 (default) on.
+"""
+
+from __future__ import annotations
+
+import os
+from typing import Generator, List, Sequence
+
+import torch
+
+_MODE = os.environ.get("NXD_SP_STREAMS", "2")
+_active = False           # inside an interleaved forward/backward (set until join())
+_streams = {}             # device index -> [stream A, stream B]
+
+
+def enabled() -> bool:
+    return _MODE == "2"
+
+
+def set_enabled(on: bool) -> None:
+    global _MODE
+    _MODE = "2" if on else "1"
+
+
+def active() -> bool:
+    return _active
+
+
+def streams_for(device: torch.device) -> List[torch.cuda.Stream]:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _streams.get(idx)
+    if s is None:
+        s = _streams[idx] = [torch.cuda.Stream(device=idx), torch.cuda.Stream(device=idx)]
+    return s
+
+
+def run_interleaved(gens: Sequence[Generator], device: torch.device) -> list:
+    """Drive the generators alternately (one step each in turn) until all return; generator i
+    runs on stream i (GPU) or inline (CPU).  Returns their return values."""
+    global _active
+    results = [None] * len(gens)
+    live = list(range(len(gens)))
+    cuda = device.type == "cuda"
+    if cuda:
+        main = torch.cuda.current_stream(device)
+        ss = streams_for(device)
+        for s in ss:
+            s.wait_stream(main)   # weights / zeroed grads / inputs written on the caller's stream
+        _active = True
+    while live:
+        for i in list(live):
+            try:
+                if cuda:
+                    with torch.cuda.stream(ss[i]):
+                        next(gens[i])
+                else:
+                    next(gens[i])
+            except StopIteration as e:
+                results[i] = e.value
+                live.remove(i)
+    if cuda:
+        for s in ss:
+            main.wait_stream(s)
+    return results
+
+
+def join() -> None:
+    """Make the current stream wait for both halves' streams (their backward ends there)."""
+    global _active
+    if not _active:
+        return
+    main = torch.cuda.current_stream()
+    for ss in _streams.values():
+        for s in ss:
+            main.wait_stream(s)
+    _active = False
+
+
+def accumulate_begin(p: torch.Tensor) -> None:
+    """Before a read-modify-write of p's fp32 main_grad: wait for the other stream's last one."""
+    if not _active:
+        return
+    ev = getattr(p, "_nxd_acc_ev", None)
+    if ev is not None:
+        torch.cuda.current_stream().wait_event(ev)
+
+
+def accumulate_end(p: torch.Tensor) -> None:
+    if not _active:
+        return
+    ev = getattr(p, "_nxd_acc_ev", None)
+    if ev is None:
+        ev = p._nxd_acc_ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream())

@@ -26,8 +26,12 @@ pytestmark = pytest.mark.gpu
 STEPS = 4
 
 
-def _w_train(rank, world, preset, sp, out):
+def _w_train(rank, world, preset, sp, out, streams=2):
     torch.cuda.set_device(0)
+    from neuronx_distributed_llama3_2_amd.parallel_layers import stream_split
+
+    # SP runs at DP = 1 take the two-stream half micro-batch interleaving by default (streams=2)
+    stream_split.set_enabled(streams == 2)
     from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
     from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW
     from neuronx_distributed_llama3_2_amd.parallel.grad_buffer import find_shared_params
@@ -57,9 +61,9 @@ def _w_train(rank, world, preset, sp, out):
         torch.save({"loss": losses, "gn": norms}, out)
 
 
-def _train(world, preset, sp):
+def _train(world, preset, sp, streams=2):
     d = tempfile.mkdtemp()
-    run_distributed(_w_train, world, preset, sp, os.path.join(d, "r.pt"))
+    run_distributed(_w_train, world, preset, sp, os.path.join(d, "r.pt"), streams)
     return torch.load(os.path.join(d, "r.pt"))
 
 
@@ -77,6 +81,14 @@ def _baseline(preset):
 def test_tp_training_on_one_gpu_matches_tp1(preset, tp, sp):
     a, b = _baseline(preset), _train(tp, preset, sp)
     assert a["loss"][-1] < a["loss"][0] - 0.3, a          # the fixed batch is being learned
+    for i in range(STEPS):
+        assert abs(a["loss"][i] - b["loss"][i]) < 1.5e-2 * abs(a["loss"][i]), (i, a, b)
+        assert abs(a["gn"][i] - b["gn"][i]) < 5e-2 * a["gn"][i], (i, a, b)
+
+
+def test_tp8_sp_one_stream_matches_tp1():
+    # the one-pass SP step (NXD_SP_STREAMS=1) stays covered next to the interleaved default
+    a, b = _baseline("tiny8"), _train(8, "tiny8", True, streams=1)
     for i in range(STEPS):
         assert abs(a["loss"][i] - b["loss"][i]) < 1.5e-2 * abs(a["loss"][i]), (i, a, b)
         assert abs(a["gn"][i] - b["gn"][i]) < 5e-2 * a["gn"][i], (i, a, b)

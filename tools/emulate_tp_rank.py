@@ -38,25 +38,103 @@ class _Done:
         return True
 
 
+class _Link:
+    """Optional link-time model (--link-gbps B): every collective runs on one high-priority side
+    stream (RCCL's per-communicator stream) after the producer's work, as a spin of
+    bytes-on-the-wire / B followed by its receiving-side write; the consumer waits on it.  Ring
+    bytes per rank: all-gather / reduce-scatter (n-1)/n of the full tensor, all-reduce twice that.
+    The spin occupies one workgroup, not RCCL's channel CUs: compute interference is not modelled
+    (profiles/r3_cu_interference.jsonl measures it)."""
+
+    def __init__(self, gbps: float):
+        self.bps = gbps * 1e9
+        self.stream = torch.cuda.Stream(priority=-1)
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch.cuda._sleep(10_000_000)
+        e1.record()
+        torch.cuda.synchronize()
+        self.cycles_per_s = 10_000_000 / (e0.elapsed_time(e1) / 1e3)
+        self.busy_s = 0.0
+
+    def run(self, nbytes: float, work):
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        t = nbytes / self.bps
+        self.busy_s += t
+        with torch.cuda.stream(self.stream):
+            torch.cuda._sleep(max(1, int(t * self.cycles_per_s)))
+            work()
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
+
+
+_LINK = None
+
+
+class _Pending:
+    def __init__(self, ev, tensors):
+        self.ev, self.tensors = ev, tensors
+
+    def wait(self):
+        if self.ev is not None:
+            torch.cuda.current_stream().wait_event(self.ev)
+            for t in self.tensors:   # allocated on the compute stream, written on the link stream
+                t.record_stream(torch.cuda.current_stream())
+            self.ev = None
+        return True
+
+    def is_completed(self):
+        return self.ev is None or self.ev.query()
+
+
+def _collective(nbytes, work, async_op, tensors):
+    if _LINK is None or not tensors[0].is_cuda:
+        work()
+        return _Done() if async_op else None
+    for t in tensors:
+        t.record_stream(_LINK.stream)
+    h = _Pending(_LINK.run(nbytes, work), tensors)
+    if async_op:
+        return h
+    h.wait()
+    return None
+
+
 def _emulate_collectives():
-    """Receiving-side HBM work of each collective, no links (see module docstring)."""
+    """Receiving-side HBM work of each collective, no links unless --link-gbps (module docstring)."""
 
     def all_gather_into_tensor(out, inp, group=None, async_op=False):
         ws = dist.get_world_size(group=group)
         inp = inp.contiguous()
-        out.view((ws,) + tuple(inp.shape)).copy_(inp.unsqueeze(0).expand((ws,) + tuple(inp.shape)))
-        return _Done() if async_op else None
+
+        def work():
+            out.view((ws,) + tuple(inp.shape)).copy_(inp.unsqueeze(0).expand((ws,) + tuple(inp.shape)))
+
+        return _collective(out.numel() * out.element_size() * (ws - 1) / ws, work, async_op, [out, inp])
 
     def reduce_scatter_tensor(out, inp, group=None, async_op=False, op=dist.ReduceOp.SUM):
         ws = dist.get_world_size(group=group)
-        out.copy_(inp.contiguous().view((ws,) + tuple(out.shape))[0])
-        return _Done() if async_op else None
+        inp = inp.contiguous()
+
+        def work():
+            out.copy_(inp.view((ws,) + tuple(out.shape))[0])
+
+        return _collective(inp.numel() * inp.element_size() * (ws - 1) / ws, work, async_op, [out, inp])
 
     def all_reduce(t, group=None, async_op=False, op=dist.ReduceOp.SUM):
-        return _Done() if async_op else None
+        ws = dist.get_world_size(group=group)
+        return _collective(2 * t.numel() * t.element_size() * (ws - 1) / ws, lambda: None, async_op, [t])
 
     def all_reduce_coalesced(tensors, group=None):
-        return None
+        tensors = [t for t in tensors if t.numel()]
+        if tensors:
+            ws = dist.get_world_size(group=group)
+            nbytes = sum(2 * t.numel() * t.element_size() * (ws - 1) / ws for t in tensors)
+            _collective(nbytes, lambda: None, False, tensors)
 
     comm.all_gather_into_tensor = all_gather_into_tensor
     comm.reduce_scatter_tensor = reduce_scatter_tensor
@@ -77,6 +155,8 @@ def main():
     ap.add_argument("--no-sp", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="plumbing check on the CPU (tiny models)")
     ap.add_argument("--hidden", type=int, default=None, help="(CPU plumbing) override hidden size")
+    ap.add_argument("--link-gbps", type=float, default=None,
+                    help="model collective time at this per-rank ring bandwidth (GB/s) on a side stream")
     a = ap.parse_args()
 
     from torch.testing._internal.distributed.fake_pg import FakeStore
@@ -94,6 +174,9 @@ def main():
         torch.cuda.set_device(0)
     dist.init_process_group("fake", rank=0, world_size=a.tp, store=FakeStore())
     _emulate_collectives()
+    global _LINK
+    if a.link_gbps and use_cuda:
+        _LINK = _Link(a.link_gbps)
     ps.initialize_model_parallel(tensor_model_parallel_size=a.tp)
     model_parallel_manual_seed(1234)
     over = dict(sequence_parallel_enabled=(a.tp > 1 and not a.no_sp), max_position_embeddings=max(8192, a.seq))
@@ -138,6 +221,9 @@ def main():
     el = (time.perf_counter() - t0) / a.steps
     rec = {"tool": "emulate_tp_rank", "tp": a.tp, "sp": over["sequence_parallel_enabled"], "model": a.model,
            "layers": cfg.num_hidden_layers, "seq": a.seq, "mbs": mbs, "gbs": a.gbs, "grad_accum": accum,
+           "sp_chunks": __import__("neuronx_distributed_llama3_2_amd.parallel_layers.sp", fromlist=["x"])
+           .get_sequence_parallel_chunks(a.tp), "link_gbps": a.link_gbps,
+           "link_busy_ms_per_step": round(1000 * _LINK.busy_s / (a.warmup + a.steps), 2) if _LINK else None,
            "ms_per_step": round(1000 * el, 2), "ms_per_microbatch": round(1000 * el / accum, 2),
            "node_tokens_per_s_comm_free": round(a.gbs * a.seq / el, 1),
            "params_per_rank": sum(p.numel() for p in model.parameters()),
