@@ -297,6 +297,7 @@ class LlamaForCausalLM(nn.Module):
         interleaved (parallel_layers/stream_split.py); same loss as the one-pass forward."""
         h = input_ids.shape[0] // 2
         am = (attention_mask[:h], attention_mask[h:]) if attention_mask is not None else (None, None)
+        self.model.rope_cache.tables(input_ids.device)   # built once on this stream, read by both halves
         gens = [self._half(input_ids[:h], labels[:h], am[0]), self._half(input_ids[h:], labels[h:], am[1])]
         (s0, n0), (s1, n1) = stream_split.run_interleaved(gens, input_ids.device)
         if input_ids.is_cuda:

@@ -30,7 +30,13 @@ class EmbeddingFunc(torch.autograd.Function):
         w = ctx.weight
         mg = getattr(w, "main_grad", None)
         dw = mg if mg is not None else torch.zeros(w.shape, dtype=torch.float32, device=w.device)
+        if mg is not None:   # atomics, but a tied lm_head's GEMM read-modify-writes the same buffer
+            from ..parallel_layers import stream_split
+
+            stream_split.accumulate_begin(w)
         ext().embedding_bwd(idc, dout.contiguous(), dw.view(w.shape), int(ctx.vocab_start))
+        if mg is not None:
+            stream_split.accumulate_end(w)
         if mg is not None:
             cb = getattr(w, "_nxd_grad_ready", None)
             if cb is not None:

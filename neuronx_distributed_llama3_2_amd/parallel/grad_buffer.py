@@ -148,7 +148,11 @@ class FlatBuffer:
     # ---------------------------------------------------------------- grad readiness / comm
     def _post_accumulate(self, p):
         if p.grad is not None:
+            from ..parallel_layers import stream_split   # (lazy: parallel_layers imports this module)
+
+            stream_split.accumulate_begin(p)
             p.main_grad.add_(p.grad.float() if p.main_grad.dtype == torch.float32 else p.grad)
+            stream_split.accumulate_end(p)
             p.grad = None
         self._on_grad_ready(p)
 
