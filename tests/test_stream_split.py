@@ -10,7 +10,7 @@ import torch
 from dist_utils import run_distributed
 
 
-def _w(rank, world, streams, out):
+def _w(rank, world, streams, out, preset="tiny8"):
     from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
     from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW
     from neuronx_distributed_llama3_2_amd.parallel.grad_buffer import find_shared_params
@@ -19,7 +19,7 @@ def _w(rank, world, streams, out):
 
     stream_split.set_enabled(streams == 2)
     ps.initialize_model_parallel(world)
-    cfg = llama_config("tiny8", sequence_parallel_enabled=True, max_position_embeddings=128, num_hidden_layers=2)
+    cfg = llama_config(preset, sequence_parallel_enabled=True, max_position_embeddings=128, num_hidden_layers=2)
     torch.manual_seed(0)
     model = LlamaForCausalLM(cfg, dtype=torch.float32, device=torch.device("cpu"))
     model.train()
@@ -48,15 +48,24 @@ def _w(rank, world, streams, out):
         torch.save({"loss": losses, "gn": norms, "interleaved": len(calls)}, out)
 
 
-def _run(world, streams):
+def _run(world, streams, preset="tiny8"):
     d = tempfile.mkdtemp()
-    run_distributed(_w, world, streams, os.path.join(d, "r.pt"))
+    run_distributed(_w, world, streams, os.path.join(d, "r.pt"), preset)
     return torch.load(os.path.join(d, "r.pt"))
 
 
 def test_interleaved_halves_match_one_pass_tp2():
     a, b = _run(2, 1), _run(2, 2)
     assert a["interleaved"] == 0 and b["interleaved"] == 3
+    for i in range(3):
+        assert abs(a["loss"][i] - b["loss"][i]) < 1e-4 * abs(a["loss"][i]), (a, b)
+        assert abs(a["gn"][i] - b["gn"][i]) < 1e-3 * a["gn"][i], (a, b)
+
+
+def test_interleaved_halves_match_one_pass_tp4_replicated_kv():
+    # tiny: 2 kv heads at TP=4 -> kv heads replicated on 2 ranks (KV-group all-reduce in backward)
+    a, b = _run(4, 1, "tiny"), _run(4, 2, "tiny")
+    assert b["interleaved"] == 3
     for i in range(3):
         assert abs(a["loss"][i] - b["loss"][i]) < 1e-4 * abs(a["loss"][i]), (a, b)
         assert abs(a["gn"][i] - b["gn"][i]) < 1e-3 * a["gn"][i], (a, b)
