@@ -19,8 +19,8 @@ _ENABLED = os.environ.get("NXD_TUNED_GEMM", "1") == "1"
 def set_overlap_safe(enabled: bool) -> None:
     """Select GEMM solutions without stream-K (csrc/gemm.cpp `no_streamk`): a persistent stream-K
     GEMM stalls while a concurrent collective holds one of its CUs.  Multi-rank training turns it
-    on (parallel_state.initialize_model_parallel) unless NXD_GEMM_NO_STREAMK is set."""
-    if "NXD_GEMM_NO_STREAMK" in os.environ or not torch.cuda.is_available():
+    on with NXD_GEMM_NO_STREAMK=1 (parallel_state.initialize_model_parallel)."""
+    if not torch.cuda.is_available():
         return
     try:
         ext().gemm_set_no_streamk(1 if enabled else 0)

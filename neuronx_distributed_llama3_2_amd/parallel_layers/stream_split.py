@@ -23,7 +23,10 @@ Shared state the two streams write is serialised here:
 
 Active only while training with TP > 1, sequence parallelism, DP = 1 (the backward-overlapped DP
 bucket reduction counts one gradient report per parameter) and no full activation checkpointing;
-NXD_SP_STREAMS=1 turns it off, =2 (default) on.
+NXD_SP_STREAMS=2 turns it on; off (1) by default until it has run on a multi-GPU node: on the one-GPU
+gloo rehearsal it matches the one-pass step in fp32 on the CPU (tests/test_stream_split.py) and in the
+GPU TP=8 parity test, but the TP=4 replicated-kv GPU run varied from run to run
+(profiles/r3_sp_streams_noise_nosk_exhaustive.jsonl, taken together with the exhaustive GEMM search).
 """
 
 from __future__ import annotations
@@ -33,7 +36,7 @@ from typing import Generator, List, Sequence
 
 import torch
 
-_MODE = os.environ.get("NXD_SP_STREAMS", "2")
+_MODE = os.environ.get("NXD_SP_STREAMS", "1")
 _active = False           # inside an interleaved forward/backward (set until join())
 _streams = {}             # device index -> [stream A, stream B]
 

@@ -26,11 +26,11 @@ pytestmark = pytest.mark.gpu
 STEPS = 4
 
 
-def _w_train(rank, world, preset, sp, out, streams=2):
+def _w_train(rank, world, preset, sp, out, streams=1):
     torch.cuda.set_device(0)
     from neuronx_distributed_llama3_2_amd.parallel_layers import stream_split
 
-    # SP runs at DP = 1 take the two-stream half micro-batch interleaving by default (streams=2)
+    # streams=2: the two-stream SP half micro-batch interleaving (NXD_SP_STREAMS=2, opt-in)
     stream_split.set_enabled(streams == 2)
     from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
     from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW
@@ -61,7 +61,7 @@ def _w_train(rank, world, preset, sp, out, streams=2):
         torch.save({"loss": losses, "gn": norms}, out)
 
 
-def _train(world, preset, sp, streams=2):
+def _train(world, preset, sp, streams=1):
     d = tempfile.mkdtemp()
     run_distributed(_w_train, world, preset, sp, os.path.join(d, "r.pt"), streams)
     return torch.load(os.path.join(d, "r.pt"))
@@ -86,9 +86,9 @@ def test_tp_training_on_one_gpu_matches_tp1(preset, tp, sp):
         assert abs(a["gn"][i] - b["gn"][i]) < 5e-2 * a["gn"][i], (i, a, b)
 
 
-def test_tp8_sp_one_stream_matches_tp1():
-    # the one-pass SP step (NXD_SP_STREAMS=1) stays covered next to the interleaved default
-    a, b = _baseline("tiny8"), _train(8, "tiny8", True, streams=1)
+def test_tp8_sp_two_stream_halves_match_tp1():
+    # the opt-in two-stream SP halves (NXD_SP_STREAMS=2) at the headline head layout
+    a, b = _baseline("tiny8"), _train(8, "tiny8", True, streams=2)
     for i in range(STEPS):
         assert abs(a["loss"][i] - b["loss"][i]) < 1.5e-2 * abs(a["loss"][i]), (i, a, b)
         assert abs(a["gn"][i] - b["gn"][i]) < 5e-2 * a["gn"][i], (i, a, b)
