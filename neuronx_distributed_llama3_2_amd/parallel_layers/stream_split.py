@@ -23,10 +23,13 @@ Shared state the two streams write is serialised here:
 
 Active only while training with TP > 1, sequence parallelism, DP = 1 (the backward-overlapped DP
 bucket reduction counts one gradient report per parameter) and no full activation checkpointing;
-NXD_SP_STREAMS=2 turns it on; off (1) by default until it has run on a multi-GPU node: on the one-GPU
-gloo rehearsal it matches the one-pass step in fp32 on the CPU (tests/test_stream_split.py) and in the
-GPU TP=8 parity test, but the TP=4 replicated-kv GPU run varied from run to run
-(profiles/r3_sp_streams_noise_nosk_exhaustive.jsonl, taken together with the exhaustive GEMM search).
+NXD_SP_STREAMS=2 turns it on; off (1) by default until it has run on a multi-GPU node.  Checked:
+fp32 CPU parity with the one-pass step (tests/test_stream_split.py, TP=2 and TP=4 replicated kv);
+on the GPU kernels (one-GPU gloo rehearsal, TP=4 replicated kv, 4 AdamW steps, three runs each)
+bit-identical from run to run and within 3e-4 of the one-pass losses / grad norms
+(profiles/r3_sp_streams_noise_default_gemm.jsonl).  The run-to-run variation first seen there came
+from the (then unvalidated) exhaustive GEMM search, not from the streams
+(profiles/r3_sp_streams_noise_nosk_exhaustive.jsonl).
 """
 
 from __future__ import annotations
