@@ -32,6 +32,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # library log records go to stderr: stdout carries exactly one line, the JSON result
 os.environ.setdefault("NXD_LOG_STREAM", "stderr")
+# TP + SP runs (N > 1): each micro-batch as two half batches on two HIP streams with their
+# collectives interleaved (parallel_layers/stream_split.py; emulated TP=8 rank at 400 GB/s per rank:
+# 601 -> 532 ms per step, TP=2 over its one xGMI link 4488 -> 1839; bit-identical across runs on the
+# GPU kernels).  Library default is one pass; NXD_SP_STREAMS=1 restores it here.
+os.environ.setdefault("NXD_SP_STREAMS", "2")
 
 # Micro-batch per TP degree: TP shrinks every per-rank GEMM and the attention head count, so the
 # TP>1 ranks process several sequences per micro-batch to keep MFMA tiles and the attention grid
