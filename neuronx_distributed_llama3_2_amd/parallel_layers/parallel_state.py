@@ -119,9 +119,8 @@ def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_mode
     from ..parallel.rccl_env import log_comm_config
 
     log_comm_config()
-    # NXD_GEMM_NO_STREAMK=1: GEMM solutions without stream-K for runs whose collectives overlap GEMMs
-    # (opt-in: its exhaustive search is validated against the heuristic result per candidate, but the
-    # first multi-rank GPU runs with it showed non-finite losses before that check existed)
+    # NXD_GEMM_NO_STREAMK=1: skip stream-K solutions of the heuristic list for runs whose
+    # collectives overlap GEMMs (opt-in; csrc/gemm.cpp)
     set_overlap_safe(os.environ.get("NXD_GEMM_NO_STREAMK", "0") == "1" and world > 1)
     _TP_GROUP = _assign(tp_mesh, rank, high_priority=True)
     _DP_GROUP = _assign(dp_mesh, rank)
