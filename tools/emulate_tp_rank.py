@@ -43,20 +43,38 @@ class _Link:
     stream (RCCL's per-communicator stream) after the producer's work, as a spin of
     bytes-on-the-wire / B followed by its receiving-side write; the consumer waits on it.  Ring
     bytes per rank: all-gather / reduce-scatter (n-1)/n of the full tensor, all-reduce twice that.
-    The spin occupies one workgroup, not RCCL's channel CUs: compute interference is not modelled
-    (profiles/r3_cu_interference.jsonl measures it)."""
 
-    def __init__(self, gbps: float):
+    The spin is csrc/diag.hip `cu_stream`: `--link-cus K` workgroups (default 1; RCCL runs one per
+    channel) stream a small buffer until the 100 MHz real-time counter has advanced by the link
+    time -- wall-clock based, so it is not stretched when the shader clock drops under MFMA load
+    (the round-3 model spun torch.cuda._sleep on the shader-clock cycle counter, calibrated idle).
+
+    Buffer lifetime (--sync stash, default): the collective's tensors are held by the handle until
+    wait() has made the consumer's stream wait for the link stream, then dropped -- what
+    ProcessGroupNCCL does with TORCH_NCCL_AVOID_RECORD_STREAMS=1 (parallel/rccl_env.py).  --sync
+    record reproduces the round-3 model: record_stream() onto the link stream, which keeps every
+    freed block out of the allocator until the GPU has passed an event the CPU enqueued far ahead
+    (profiles/r4_emulate_stall.jsonl measures what that did)."""
+
+    def __init__(self, gbps: float, cus: int = 1, spin: str = "realtime"):
+        from neuronx_distributed_llama3_2_amd.ops import ext
+
+        self.C = ext()
+        self.spin = spin
+        if spin == "sleep":   # round-3 model: shader-clock cycles, calibrated on an idle GPU
+            torch.cuda._sleep(1000)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            torch.cuda._sleep(10_000_000)
+            e1.record()
+            torch.cuda.synchronize()
+            self.cycles_per_s = 10_000_000 / (e0.elapsed_time(e1) / 1e3)
         self.bps = gbps * 1e9
+        self.cus = max(1, int(cus))
         self.stream = torch.cuda.Stream(priority=-1)
-        torch.cuda._sleep(1000)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        torch.cuda._sleep(10_000_000)
-        e1.record()
-        torch.cuda.synchronize()
-        self.cycles_per_s = 10_000_000 / (e0.elapsed_time(e1) / 1e3)
+        self.src = torch.zeros(self.cus * 4096, dtype=torch.uint8, device="cuda")
+        self.dst = torch.empty_like(self.src)
         self.busy_s = 0.0
 
     def run(self, nbytes: float, work):
@@ -65,7 +83,10 @@ class _Link:
         t = nbytes / self.bps
         self.busy_s += t
         with torch.cuda.stream(self.stream):
-            torch.cuda._sleep(max(1, int(t * self.cycles_per_s)))
+            if self.spin == "sleep":
+                torch.cuda._sleep(max(1, int(t * self.cycles_per_s)))
+            else:
+                self.C.cu_stream(self.src, self.dst, 4096, self.cus, max(1, int(t * 1e8)))
             work()
         ev = torch.cuda.Event()
         ev.record(self.stream)
@@ -73,6 +94,7 @@ class _Link:
 
 
 _LINK = None
+_SYNC = "stash"
 
 
 class _Pending:
@@ -82,9 +104,11 @@ class _Pending:
     def wait(self):
         if self.ev is not None:
             torch.cuda.current_stream().wait_event(self.ev)
-            for t in self.tensors:   # allocated on the compute stream, written on the link stream
-                t.record_stream(torch.cuda.current_stream())
+            if _SYNC == "record":   # allocated on the compute stream, written on the link stream
+                for t in self.tensors:
+                    t.record_stream(torch.cuda.current_stream())
             self.ev = None
+            self.tensors = None     # stash released: the consumer's stream is now ordered after the link
         return True
 
     def is_completed(self):
@@ -95,8 +119,9 @@ def _collective(nbytes, work, async_op, tensors):
     if _LINK is None or not tensors[0].is_cuda:
         work()
         return _Done() if async_op else None
-    for t in tensors:
-        t.record_stream(_LINK.stream)
+    if _SYNC == "record":
+        for t in tensors:
+            t.record_stream(_LINK.stream)
     h = _Pending(_LINK.run(nbytes, work), tensors)
     if async_op:
         return h
@@ -157,6 +182,12 @@ def main():
     ap.add_argument("--hidden", type=int, default=None, help="(CPU plumbing) override hidden size")
     ap.add_argument("--link-gbps", type=float, default=None,
                     help="model collective time at this per-rank ring bandwidth (GB/s) on a side stream")
+    ap.add_argument("--link-cus", type=int, default=1, help="workgroups the link spin occupies (RCCL channels)")
+    ap.add_argument("--sync", choices=["stash", "record"], default="stash",
+                    help="collective buffer lifetime: stash until wait() (RCCL default) or record_stream")
+    ap.add_argument("--spin", choices=["realtime", "sleep"], default="realtime",
+                    help="link spin: real-time-counter copy kernel, or round-3's torch.cuda._sleep")
+    ap.add_argument("--sp-streams", type=int, default=None, help="NXD_SP_STREAMS for this run (1 or 2)")
     a = ap.parse_args()
 
     from torch.testing._internal.distributed.fake_pg import FakeStore
@@ -174,9 +205,14 @@ def main():
         torch.cuda.set_device(0)
     dist.init_process_group("fake", rank=0, world_size=a.tp, store=FakeStore())
     _emulate_collectives()
-    global _LINK
+    global _LINK, _SYNC
+    _SYNC = a.sync
+    if a.sp_streams is not None:
+        from neuronx_distributed_llama3_2_amd.parallel_layers import stream_split
+
+        stream_split.set_enabled(a.sp_streams == 2)
     if a.link_gbps and use_cuda:
-        _LINK = _Link(a.link_gbps)
+        _LINK = _Link(a.link_gbps, a.link_cus, a.spin)
     ps.initialize_model_parallel(tensor_model_parallel_size=a.tp)
     model_parallel_manual_seed(1234)
     over = dict(sequence_parallel_enabled=(a.tp > 1 and not a.no_sp), max_position_embeddings=max(8192, a.seq))
@@ -213,21 +249,34 @@ def main():
         step()
     if use_cuda:
         torch.cuda.synchronize()
+        ms0 = torch.cuda.memory_stats(dev)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     if use_cuda:
         torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / a.steps
+    mem = {}
+    if use_cuda:
+        ms1 = torch.cuda.memory_stats(dev)
+        # allocator events inside the timed steps (retries = OOM -> free cached blocks -> retry,
+        # each a device-wide synchronisation; device allocs = fresh hipMalloc calls)
+        mem = {k: ms1.get(k, 0) - ms0.get(k, 0) for k in ("num_alloc_retries", "num_sync_all_streams",
+                                                            "num_device_alloc", "num_device_free")}
+        mem["num_alloc_retries_total"] = ms1.get("num_alloc_retries", 0)
+        mem["peak_reserved_gib"] = round(torch.cuda.max_memory_reserved(dev) / 2**30, 1)
     rec = {"tool": "emulate_tp_rank", "tp": a.tp, "sp": over["sequence_parallel_enabled"], "model": a.model,
            "layers": cfg.num_hidden_layers, "seq": a.seq, "mbs": mbs, "gbs": a.gbs, "grad_accum": accum,
            "sp_chunks": __import__("neuronx_distributed_llama3_2_amd.parallel_layers.sp", fromlist=["x"])
            .get_sequence_parallel_chunks(a.tp), "link_gbps": a.link_gbps,
+           "link_cus": a.link_cus if _LINK else None, "spin": a.spin if _LINK else None, "sync": a.sync,
+           "sp_streams": 2 if __import__("neuronx_distributed_llama3_2_amd.parallel_layers.stream_split",
+                                          fromlist=["x"]).enabled() else 1,
            "link_busy_ms_per_step": round(1000 * _LINK.busy_s / (a.warmup + a.steps), 2) if _LINK else None,
            "ms_per_step": round(1000 * el, 2), "ms_per_microbatch": round(1000 * el / accum, 2),
            "node_tokens_per_s_comm_free": round(a.gbs * a.seq / el, 1),
            "params_per_rank": sum(p.numel() for p in model.parameters()),
-           "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if use_cuda else 0.0}
+           "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if use_cuda else 0.0, **mem}
     print(json.dumps(rec), flush=True)
     dist.destroy_process_group()
 
