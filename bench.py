@@ -111,9 +111,13 @@ def launch_local_ranks(argv, n: int) -> int:
     return rc
 
 
-def _build_pipeline(a, cfg, tp, n_micro, dev, dtype):
-    """NxDPPModel (1F1B over `n_micro` micro-batches, even layer split) + the trainer's optimizer
-    (fp32 master weights, ZeRO-1 over DP) through the public training API."""
+def _build(a, cfg, tp, n_micro, dev, dtype):
+    """Model + optimizer through the public training API, as the reference's headline script builds
+    them (examples/training/llama/tp_zero1_llama_hf_pretrain/tp_zero1_llama_hf_pretrain.py:191-238):
+    `neuronx_distributed_config` -> `initialize_parallel_model` -> `initialize_parallel_optimizer`
+    with ZeRO-1 + fp32 master weights + fp32 gradient accumulation (the flat fused-AdamW optimizer;
+    ZeRO-1 over DP).  --pp P > 1 wraps the model in NxDPPModel (1F1B over `n_micro` micro-batches,
+    even layer split)."""
     import torch
 
     import neuronx_distributed_llama3_2_amd as nxd
@@ -121,10 +125,12 @@ def _build_pipeline(a, cfg, tp, n_micro, dev, dtype):
     from neuronx_distributed_llama3_2_amd.parallel_layers import parallel_state as ps
     from neuronx_distributed_llama3_2_amd.utils.training_utils import create_partition, get_param_groups_by_weight_decay
 
-    cuts = create_partition(cfg.num_hidden_layers, a.pp)
-    pcfg = {"transformer_layer_cls": LlamaDecoderLayer, "num_microbatches": n_micro, "virtual_pipeline_size": 1,
-            "input_names": ["input_ids", "labels"], "broadcast_and_average_loss": True,
-            "auto_partition": False, "pipeline_cuts": cuts}
+    pcfg = None
+    if a.pp > 1:
+        cuts = create_partition(cfg.num_hidden_layers, a.pp)
+        pcfg = {"transformer_layer_cls": LlamaDecoderLayer, "num_microbatches": n_micro, "virtual_pipeline_size": 1,
+                "input_names": ["input_ids", "labels"], "broadcast_and_average_loss": True,
+                "auto_partition": False, "pipeline_cuts": cuts}
     nxd_config = nxd.neuronx_distributed_config(
         tensor_parallel_size=tp, pipeline_parallel_size=a.pp, pipeline_config=pcfg,
         sequence_parallel=cfg.sequence_parallel_enabled,
@@ -138,14 +144,29 @@ def _build_pipeline(a, cfg, tp, n_micro, dev, dtype):
     return model, opt
 
 
+def _arm_watchdog(rank: int, timeout_s: float):
+    """Host-side heartbeat (kicked every micro-step): if no progress for `timeout_s` -- a hung
+    collective, a rank that died -- dump every thread's stack and this rank's last collectives
+    (parallel/comm.py flight recorder) to stderr and exit 124, well inside the driver's limit."""
+    from neuronx_distributed_llama3_2_amd.parallel import comm
+    from neuronx_distributed_llama3_2_amd.utils.resilience import StepWatchdog
+
+    def dump():
+        sys.stderr.write(f"[bench] rank {rank}: last collectives issued:\n  " + "\n  ".join(comm.flight_record(16))
+                         + "\n")
+        sys.stderr.flush()
+
+    return StepWatchdog(timeout_s, on_timeout=dump, exit_on_timeout=True, exit_code=124)
+
+
 def main(a):
     import torch
     import torch.distributed as dist
 
-    from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
-    from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW
-    from neuronx_distributed_llama3_2_amd.parallel.grad_buffer import find_shared_params
+    from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import llama_config
     from neuronx_distributed_llama3_2_amd.parallel_layers import parallel_state as ps
+    from neuronx_distributed_llama3_2_amd.parallel_layers import stream_split
+    from neuronx_distributed_llama3_2_amd.utils.resilience import configure_collective_watchdog, fault_point
     from neuronx_distributed_llama3_2_amd.parallel_layers.random import model_parallel_manual_seed
     from neuronx_distributed_llama3_2_amd.utils.profiling import llama_num_params, mfu, model_flops_per_token
 
@@ -170,8 +191,13 @@ def main(a):
     from neuronx_distributed_llama3_2_amd.parallel.rccl_env import apply_rccl_env
 
     apply_rccl_env()
-    dist.init_process_group(backend, rank=rank, world_size=world,
+    # a failed / timed-out RCCL collective tears the process down (TORCH_NCCL_ASYNC_ERROR_HANDLING)
+    # instead of hanging every rank; the host watchdog below catches what that does not
+    wd_s = float(os.environ.get("NXD_BENCH_WATCHDOG_S", "300"))
+    coll_timeout = configure_collective_watchdog(2 * wd_s)
+    dist.init_process_group(backend, rank=rank, world_size=world, timeout=coll_timeout,
                             device_id=torch.device("cuda", local_rank) if use_cuda and backend == "nccl" else None)
+    watchdog = _arm_watchdog(rank, wd_s) if wd_s > 0 else None
     dev = torch.device("cuda", local_rank) if use_cuda else torch.device("cpu")
     # preflight: one all-reduce over the whole job must see every rank (RCCL on GPU)
     probe = torch.ones(1, device=dev)
@@ -208,17 +234,8 @@ def main(a):
     if a.gbs % (a.mbs * dp):
         raise SystemExit(f"bench: global batch {a.gbs} not divisible by micro-batch {a.mbs} x DP {dp}")
     accum = a.gbs // (a.mbs * dp)
-    if a.pp > 1:
-        model, opt = _build_pipeline(a, cfg, tp, accum, dev, torch.bfloat16)
-        dp = ps.get_data_parallel_size()
-    else:
-        model = LlamaForCausalLM(cfg, dtype=torch.bfloat16, device=dev)
-        model.train()
-        decay = [p for n, p in model.named_parameters() if p.dim() > 1]
-        no_decay = [p for n, p in model.named_parameters() if p.dim() <= 1]
-        opt = FlatMixedPrecisionAdamW([{"params": decay, "weight_decay": 0.01}, {"params": no_decay, "weight_decay": 0.0}],
-                                      lr=a.lr, betas=(0.9, 0.95), eps=1e-8, zero1=dp > 1, grad_clipping=True,
-                                      max_grad_norm=1.0, shared_param_ids=find_shared_params(model))
+    model, opt = _build(a, cfg, tp, accum, dev, torch.bfloat16)
+    dp = ps.get_data_parallel_size()
     nparams_local = sum(p.numel() for p in model.parameters())
     # a fresh batch for every micro-step of every step (warmup included), generated before the timed
     # region; identical across the TP ranks of one DP rank.  Random tokens cannot be memorised, so
@@ -248,24 +265,33 @@ def main(a):
             opt.set_grad_sync(i == accum - 1)
             ids = batches[cursor[0]]
             cursor[0] += 1
+            fault_point("bench_microstep")   # NXD_FAULT_INJECT test site (watchdog exit path)
             out = model(ids, labels=ids)
             (out.loss / accum).backward()
             tot = out.loss.detach() if tot is None else tot + out.loss.detach()
+            if watchdog is not None:
+                watchdog.kick()
         opt.step()
         opt.zero_grad()
         return tot / accum   # mean over the step's micro-batches (= the pipeline path's loss)
 
     for _ in range(a.warmup):
         loss = train_step()
+        if watchdog is not None:
+            watchdog.kick()
     if use_cuda:
         torch.cuda.synchronize()
     dist.barrier()
+    ms0 = torch.cuda.memory_stats(dev) if use_cuda else {}
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = train_step()
+        if watchdog is not None:
+            watchdog.kick()
     if use_cuda:
         torch.cuda.synchronize()
     dist.barrier()
+    ms1 = torch.cuda.memory_stats(dev) if use_cuda else {}
     elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     el = float(elapsed.item())
@@ -305,8 +331,15 @@ def main(a):
             "mfu": round(mfu(value, fpt, world), 4),   # vs 2.5 PFLOP/s dense bf16 per GPU
             "peak_mem_gib": round(mem, 1),
             "peak_reserved_gib": round(torch.cuda.max_memory_reserved(dev) / 2**30, 1) if use_cuda else 0.0,
+            # caching-allocator events inside the timed steps (a retry = OOM -> free cache -> device sync)
+            "num_alloc_retries": int(ms1.get("num_alloc_retries", 0) - ms0.get("num_alloc_retries", 0)),
+            "rccl_max_channels": os.environ.get("NCCL_MAX_NCHANNELS", "rccl default"),
+            "sp_streams": 2 if stream_split.enabled() and over["sequence_parallel_enabled"] else 1,
+            "api": "nxd.initialize_parallel_model / initialize_parallel_optimizer",
         }
         print(json.dumps(rec), flush=True)
+    if watchdog is not None:
+        watchdog.stop()
     dist.barrier()
     dist.destroy_process_group()
 

@@ -50,10 +50,16 @@ struct Problem {
   int ta, tc;               // input / output hipDataType
   int beta_nonzero;
   bool no_sk = false;
+  bool in_place = false;    // C and D are the same memory (the fp32 main_grad accumulation)
+  int align = 256;          // smallest power-of-two alignment (<= 256 B) of the A / B / C / D pointers
   std::string key() const {
     std::ostringstream s;
     s << opA << ' ' << opB << ' ' << m << ' ' << n << ' ' << k << ' ' << lda << ' ' << ldb << ' ' << ldc << ' ' << ldd
       << ' ' << ta << ' ' << tc << ' ' << beta_nonzero << (no_sk ? " nosk" : "");
+    // a solution validated at one pointer alignment / aliasing is not assumed valid at another
+    // (the exhaustive search's choices are checked on exactly this call's layout)
+    if (align < 256) s << " al" << align;
+    if (beta_nonzero && in_place) s << " ip";
     return s.str();
   }
 };
@@ -268,6 +274,23 @@ static void transposed_view(const at::Tensor& x, int64_t* rows, int64_t* cols, i
   }
 }
 
+static int ptr_align(const void* p) {
+  const uintptr_t v = (uintptr_t)p;
+  int a = 256;
+  while (a > 1 && (v % a)) a >>= 1;
+  return a;
+}
+
+// A scratch tensor shaped / strided like `like` whose data pointer has the same alignment mod
+// 256 B: exhaustive candidates are validated at the production call's alignment.
+static at::Tensor scratch_like(const at::Tensor& like) {
+  const int64_t es = like.element_size();
+  const int64_t off = (int64_t)(((uintptr_t)like.data_ptr()) % 256) / es;
+  const int64_t span = like.size(0) > 0 ? (like.size(0) - 1) * like.stride(0) + like.size(1) : 0;
+  at::Tensor buf = at::empty({span + 256 / es}, like.options());
+  return buf.as_strided(like.sizes(), like.strides(), off);
+}
+
 static bool capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(s, &st);
@@ -326,6 +349,9 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
   p.tc = dt(d);
   p.beta_nonzero = beta_d != 0.0;
   p.no_sk = no_streamk();
+  p.in_place = c.data_ptr() == d.data_ptr();
+  p.align = std::min(std::min(ptr_align(a.data_ptr()), ptr_align(b.data_ptr())),
+                     std::min(ptr_align(c.data_ptr()), ptr_align(d.data_ptr())));
   const float alpha = (float)alpha_d, beta = (float)beta_d;
   auto& T = Tuner::get();
   hipblasLtHandle_t h = T.handle();
@@ -354,27 +380,30 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
     }
   }
   if (!known && T.mode() >= 2 && !capturing(s)) {
-    // exhaustive: every library solution for this (ops, dtypes), filtered by support, timed once,
-    // the five fastest re-timed.  Experimental: in the one-GPU multi-rank rehearsal the solutions it
-    // picked gave wrong weight gradients (non-finite losses by step 2) even though each passed the
-    // reference check below at tuning time (profiles/r3_gemm_exhaustive_nosk_wrong.jsonl); the
-    // overlap-safe mode therefore only filters the heuristic list.
+    // exhaustive: every library solution for this (ops, dtypes), filtered by support, checked and
+    // timed once, the five fastest re-timed.  Each candidate runs on EXACTLY this call's layout:
+    // same D / C alignment mod 256 B, and for an in-place accumulation (C == D, the fp32 main_grad
+    // of the weight gradients) an aliased C == D scratch holding a copy of the accumulator.  In
+    // round 3 candidates were checked out of place (C != D, fresh allocator-aligned D) and some of
+    // the picks gave wrong weight gradients in place (profiles/r3_gemm_exhaustive_nosk_wrong.jsonl);
+    // tests/test_gemm_exhaustive_gpu.py runs this mode on the in-place TP=8 wgrad shapes.
     std::vector<hipblasLtMatmulHeuristicResult_t> all;
     LT_CHECK(hipblaslt_ext::getAllAlgos(h, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, (hipblasOperation_t)p.opA,
                                         (hipblasOperation_t)p.opB, (hipDataType)p.ta, (hipDataType)p.ta,
                                         (hipDataType)p.tc, (hipDataType)p.tc, HIPBLAS_COMPUTE_32F, all));
     const size_t wsmax = T.max_ws();
     void* wsp = T.workspace(wsmax, s);
-    at::Tensor scratch;
-    void* Dp = d.data_ptr();
-    if (p.beta_nonzero) {
-      scratch = at::empty_like(d);
-      Dp = scratch.data_ptr();
-    }
-    // reference result of hipBLASLt's own first heuristic choice: every exhaustive candidate's output
-    // is checked against it (a solution the library reports as supported has been seen to return
-    // non-finite values for some shapes), and a mismatching candidate is never picked
-    at::Tensor out_t = p.beta_nonzero ? scratch : d;
+    // candidate output: D-layout scratch at D's alignment; C is the same scratch when in place,
+    // else the caller's C (read only)
+    at::Tensor out_t = scratch_like(d);
+    at::Tensor c_init = p.beta_nonzero ? c.clone() : at::Tensor();   // accumulator before this call
+    void* Dp = out_t.data_ptr();
+    const void* Cp = p.in_place ? (const void*)Dp : c.data_ptr();
+    auto reset = [&]() {
+      if (p.beta_nonzero && p.in_place) out_t.copy_(c_init);
+    };
+    // reference: hipBLASLt's first heuristic choice (the default mode's path), C = c_init, D = a
+    // separate buffer
     at::Tensor ref;
     {
       hipblasLtMatmulPreference_t pref;
@@ -385,69 +414,71 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
       int got0 = 0;
       LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, ds.op, ds.A, ds.B, ds.C, ds.D, pref, 1, &r0, &got0));
       hipblasLtMatmulPreferenceDestroy(pref);
-      if (got0 > 0 && hipblasLtMatmul(h, ds.op, &alpha, b.data_ptr(), ds.A, a.data_ptr(), ds.B, &beta, c.data_ptr(),
-                                      ds.C, Dp, ds.D, &r0.algo, wsp, wsmax, s) == HIPBLAS_STATUS_SUCCESS)
-        ref = out_t.to(at::kFloat, /*non_blocking=*/false, /*copy=*/true);   // (a copy even for fp32 D)
+      at::Tensor rbuf = at::empty_like(d);
+      const void* rc = p.beta_nonzero ? c_init.data_ptr() : rbuf.data_ptr();
+      if (got0 > 0 && hipblasLtMatmul(h, ds.op, &alpha, b.data_ptr(), ds.A, a.data_ptr(), ds.B, &beta, rc, ds.C,
+                                      rbuf.data_ptr(), ds.D, &r0.algo, wsp, wsmax, s) == HIPBLAS_STATUS_SUCCESS)
+        ref = rbuf.to(at::kFloat, /*non_blocking=*/false, /*copy=*/true);
       if (ref.defined() && !at::isfinite(ref).all().item<bool>()) ref = at::Tensor();   // no usable reference
     }
     const float ref_max = ref.defined() ? ref.abs().max().item<float>() : 0.f;
-    auto matches_ref = [&]() -> bool {
+    // one untimed run from the reset state, compared with the reference
+    auto check = [&](const hipblasLtMatmulAlgo_t& algo) -> bool {
+      reset();
+      if (hipblasLtMatmul(h, ds.op, &alpha, b.data_ptr(), ds.A, a.data_ptr(), ds.B, &beta, Cp, ds.C, Dp, ds.D, &algo,
+                          wsp, wsmax, s) != HIPBLAS_STATUS_SUCCESS)
+        return false;
       if (!ref.defined()) return at::isfinite(out_t).all().item<bool>();
       const float err = (out_t.to(at::kFloat) - ref).abs().max().item<float>();   // NaN fails
       return err <= 2e-2f * ref_max + 1e-3f;
     };
     std::vector<std::pair<float, int>> timed;
     std::vector<size_t> wss(all.size(), 0);
-    int tried = 0;
-    for (size_t i = 0; i < all.size() && tried < T.max_algos(); ++i) {
-      size_t wsz = 0;
-      if (hipblaslt_ext::matmulIsAlgoSupported(h, ds.op, &alpha, ds.A, ds.B, &beta, ds.C, ds.D, all[i].algo, wsz) !=
-              HIPBLAS_STATUS_SUCCESS ||
-          wsz > wsmax || (p.no_sk && is_streamk(h, all[i].algo)))
-        continue;
-      ++tried;
-      wss[i] = wsz;
-      float ms = time_algo(h, ds, all[i].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(), c.data_ptr(), Dp, wsp, wsmax,
-                           s, 1);
-      if (ms > 0.f && matches_ref()) timed.emplace_back(ms, (int)i);
-    }
-    if (timed.empty() && p.no_sk) {  // no data-parallel solution at all: allow stream-K
-      for (size_t i = 0; i < all.size() && (int)timed.size() < T.max_algos(); ++i) {
+    auto sweep = [&](bool allow_sk) {
+      int tried = 0;
+      for (size_t i = 0; i < all.size() && tried < T.max_algos(); ++i) {
         size_t wsz = 0;
         if (hipblaslt_ext::matmulIsAlgoSupported(h, ds.op, &alpha, ds.A, ds.B, &beta, ds.C, ds.D, all[i].algo, wsz) !=
-                HIPBLAS_STATUS_SUCCESS || wsz > wsmax)
+                HIPBLAS_STATUS_SUCCESS ||
+            wsz > wsmax || (!allow_sk && is_streamk(h, all[i].algo)))
           continue;
+        ++tried;
         wss[i] = wsz;
-        float ms = time_algo(h, ds, all[i].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(), c.data_ptr(), Dp, wsp,
-                             wsmax, s, 1);
-        if (ms > 0.f && matches_ref()) timed.emplace_back(ms, (int)i);
+        if (!check(all[i].algo)) continue;
+        const float ms = time_algo(h, ds, all[i].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(), Cp, Dp, wsp, wsmax,
+                                   s, 1);
+        if (ms > 0.f) timed.emplace_back(ms, (int)i);
       }
-    }
+    };
+    sweep(!p.no_sk);
+    if (timed.empty() && p.no_sk) sweep(true);   // no data-parallel solution at all: allow stream-K
     if (!timed.empty()) {  // (nothing passed the check: the heuristic path below decides)
       std::sort(timed.begin(), timed.end());
-      int best = timed[0].second;
+      int best = -1;
       float best_ms = 1e30f;
       const double flops = 2.0 * M * N * K;
       const int reps = flops > 1e12 ? 5 : (flops > 1e10 ? 10 : 30);
       for (size_t j = 0; j < std::min<size_t>(5, timed.size()); ++j) {
         const int i = timed[j].second;
-        float ms = time_algo(h, ds, all[i].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(), c.data_ptr(), Dp, wsp, wsmax,
-                             s, reps);
-        if (ms > 0.f && ms < best_ms) {
+        float ms = time_algo(h, ds, all[i].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(), Cp, Dp, wsp, wsmax, s,
+                             reps);
+        if (ms > 0.f && ms < best_ms && check(all[i].algo)) {   // re-checked after the repeated runs
           best_ms = ms;
           best = i;
         }
       }
-      ch.algo = all[best].algo;
-      ch.ws = wss[best];
-      ch.ms = best_ms;
-      ch.index = hipblaslt_ext::getIndexFromAlgo(all[best].algo);
-      ch.resolved = true;
-      known = true;
-      T.store(key, ch, true);
-      if (std::getenv("NXD_GEMM_LOG_CHOICE"))
-        std::fprintf(stderr, "[nxd gemm] %s -> %s %.4f ms (exhaustive, %zu timed)\n", key.c_str(),
-                     hipblaslt_ext::getKernelNameFromAlgo(h, ch.algo).c_str(), best_ms, timed.size());
+      if (best >= 0) {
+        ch.algo = all[best].algo;
+        ch.ws = wss[best];
+        ch.ms = best_ms;
+        ch.index = hipblaslt_ext::getIndexFromAlgo(all[best].algo);
+        ch.resolved = true;
+        known = true;
+        T.store(key, ch, true);
+        if (std::getenv("NXD_GEMM_LOG_CHOICE"))
+          std::fprintf(stderr, "[nxd gemm] %s -> %s %.4f ms (exhaustive, %zu timed)\n", key.c_str(),
+                       hipblaslt_ext::getKernelNameFromAlgo(h, ch.algo).c_str(), best_ms, timed.size());
+      }
     }
   }
   if (!known || !ch.resolved) {

@@ -317,9 +317,23 @@ class LlamaForCausalLMInference:
         self.kv_cache_populated = True
         return logits.float()
 
+    def _graphs_allowed(self) -> bool:
+        """hipGraphs capture RCCL kernels, not host-staged gloo collectives: a TP group on gloo
+        (several ranks sharing one GPU, the single-GPU rehearsal of a TP server) runs eagerly."""
+        if not getattr(self.config, "use_hip_graphs", True) or self.device.type != "cuda":
+            return False
+        if getattr(self.config, "tp_degree", 1) > 1:
+            import torch.distributed as dist
+
+            from ..parallel_layers import parallel_state as ps
+
+            if dist.is_initialized() and ps.model_parallel_is_initialized() and \
+                    dist.get_backend(ps.get_tensor_model_parallel_group()) == "gloo":
+                return False
+        return True
+
     def _prefill_graphs_on(self) -> bool:
-        return (self.device.type == "cuda" and getattr(self.config, "prefill_graphs", True)
-                and getattr(self.config, "use_hip_graphs", True))
+        return getattr(self.config, "prefill_graphs", True) and self._graphs_allowed()
 
     def _prefill_graph(self, B: int, Tb: int) -> "PrefillGraph":
         """One captured context-encoding forward per (batch, bucket) -- the reference compiles one
@@ -369,7 +383,7 @@ class LlamaForCausalLMInference:
         g = self._graphs.get(key)
         if g is None:
             g = self._graphs[key] = DecodeGraph(self.model, sampler, self._decode_state(batch), self.graph_steps,
-                                                use_graph=self.config.use_hip_graphs)
+                                                use_graph=self._graphs_allowed())
         return g
 
     @torch.no_grad()

@@ -26,6 +26,7 @@ import torch.distributed as dist
 from .. import ops
 from ..parallel.grad_buffer import KIND_DUP_SP, KIND_SHARDED, FlatBuffer, param_kind
 from ..parallel_layers import parallel_state as ps
+from ..parallel_layers import stream_split
 from .flat_optimizer import FlatMixedPrecisionAdamW, replica_slices
 
 _ADAM_NAMES = {"AdamW", "Adam", "AdamW_FP32OptimParams", "FusedAdam"}
@@ -73,11 +74,13 @@ class _GenericZero1(torch.optim.Optimizer):
             b.set_sync(enabled)
 
     def zero_grad(self, set_to_none: bool = True) -> None:
+        stream_split.join()
         for b, _ in self.buffers:
             b.zero_grad()
 
     @torch.no_grad()
     def step(self, closure=None):
+        stream_split.join()   # main_grad is written by the SP halves' streams
         for b, _ in self.buffers:
             b.finish_grad_sync()
         tp = ps.get_tensor_model_parallel_size() if ps.model_parallel_is_initialized() else 1

@@ -28,6 +28,7 @@ bench has run; CPU / gloo tensors always take the torch path.
 
 from __future__ import annotations
 
+import collections
 import itertools
 import os
 import traceback
@@ -80,6 +81,26 @@ def _track(work, op: str, t: torch.Tensor):
 
 def pending_collectives() -> List[str]:
     return list(_pending.values())
+
+
+# Flight recorder: the last collectives this process issued (sequence number, op, shape, dtype,
+# group size), always on -- one deque append per call.  A hung job's watchdog prints it on every
+# rank (bench.py); ranks whose last sequence numbers differ are the ones that diverged.
+_FLIGHT = collections.deque(maxlen=int(os.environ.get("NXD_COMM_FLIGHT", "64")))
+_seq = itertools.count()
+
+
+def _fr(op: str, t: torch.Tensor, group) -> None:
+    try:
+        ws = dist.get_world_size(group=group)
+    except Exception:  # pragma: no cover
+        ws = -1
+    _FLIGHT.append((next(_seq), op, tuple(t.shape), str(t.dtype).replace("torch.", ""), ws))
+
+
+def flight_record(last: Optional[int] = None) -> List[str]:
+    recs = list(_FLIGHT)[-last:] if last else list(_FLIGHT)
+    return [f"#{n} {op}{shape} {dt} ws={ws}" for n, op, shape, dt, ws in recs]
 
 
 def assert_no_pending_collectives(where: str) -> None:
@@ -137,6 +158,7 @@ def _is_gloo(group) -> bool:
 
 def all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
     """out[i*n:(i+1)*n] = inp of rank i (dim 0)."""
+    _fr("all_gather", out, group)
     nc = _native_for(group, out)
     if nc is not None:
         return _native_result(nc.all_gather([out], [inp.contiguous()], async_op=async_op), async_op, "all_gather", out)
@@ -156,6 +178,7 @@ def all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, asy
 def reduce_scatter_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False,
                           op=dist.ReduceOp.SUM):
     """out = sum over ranks of inp[rank*n:(rank+1)*n] (dim 0)."""
+    _fr("reduce_scatter", inp, group)
     nc = _native_for(group, inp) if op == dist.ReduceOp.SUM else None
     if nc is not None:
         w = nc.reduce_scatter([out], [inp.contiguous()], "sum", async_op=async_op)
@@ -172,6 +195,7 @@ def reduce_scatter_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, asyn
 
 
 def all_reduce(t: torch.Tensor, group=None, async_op: bool = False, op=dist.ReduceOp.SUM):
+    _fr("all_reduce", t, group)
     nc = _native_for(group, t) if op == dist.ReduceOp.SUM and t.is_contiguous() else None
     if nc is not None:
         return _native_result(nc.all_reduce([t], "sum", async_op=async_op), async_op, "all_reduce", t)
@@ -185,6 +209,7 @@ def all_reduce_coalesced(tensors: List[torch.Tensor], group=None) -> None:
     tensors = [t for t in tensors if t.numel()]
     if not tensors or dist.get_world_size(group=group) == 1:
         return
+    _fr(f"all_reduce_coalesced[{len(tensors)}]", tensors[0], group)
     nc = _native_for(group, tensors[0]) if all(t.is_contiguous() for t in tensors) else None
     if nc is not None:
         nc.all_reduce(list(tensors), "sum", async_op=False)
@@ -201,6 +226,7 @@ def all_reduce_coalesced(tensors: List[torch.Tensor], group=None) -> None:
 
 
 def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
+    _fr("all_to_all", inp, group)
     if not _is_gloo(group):
         w = dist.all_to_all_single(out, inp.contiguous(), group=group, async_op=async_op)
         return _track(w, "all_to_all", inp) if async_op else w
@@ -225,14 +251,17 @@ def _a2a_via_gather(outs: List[torch.Tensor], ins: List[torch.Tensor], group):
 
 
 def send(t: torch.Tensor, dst: int, group=None):
+    _fr(f"send->{dst}", t, group)
     return dist.isend(t.contiguous(), dst, group=group)
 
 
 def recv(t: torch.Tensor, src: int, group=None):
+    _fr(f"recv<-{src}", t, group)
     return dist.irecv(t, src, group=group)
 
 
 def batch_isend_irecv(ops: List[dist.P2POp]):
     if not ops:
         return []
+    _fr(f"batch_p2p[{len(ops)}]", ops[0].tensor, ops[0].group)
     return dist.batch_isend_irecv(ops)

@@ -16,7 +16,7 @@ from typing import Any, Dict
 
 import torch
 
-from ..parallel_layers import parallel_state
+from ..parallel_layers import parallel_state, stream_split
 from ..parallel_layers.grads import allreduce_sequence_parallel_gradients, bucket_allreduce_gradients, clip_grad_norm
 
 
@@ -69,6 +69,9 @@ class NxDOptimizer(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        # the two sequence-parallel halves' streams (parallel_layers/stream_split.py) end the
+        # backward and write main_grad: every optimizer kind reads gradients after them
+        stream_split.join()
         if self._flat:
             return self.optimizer.step(closure)
         params = self._params()
@@ -87,6 +90,7 @@ class NxDOptimizer(torch.optim.Optimizer):
         return self.optimizer.step(closure)
 
     def zero_grad(self, set_to_none: bool = True):
+        stream_split.join()
         return self.optimizer.zero_grad(set_to_none=set_to_none)
 
     def state_dict(self):

@@ -77,3 +77,18 @@ def test_bench_pipeline_mode():
     assert rec["config"]["parallelism"] == "tp2_sp_pp2_1f1b" and rec["config"]["grad_accum"] == 4
     assert rec["n_gpus"] == 4 and rec["value"] > 0
     assert abs(rec["loss"] - math.log(1024)) < 0.5, rec["loss"]
+
+
+def test_bench_hung_rank_exits_through_watchdog():
+    """A rank that stops making progress (injected hang before its 2nd micro-step; the other rank
+    then blocks in a collective) ends the job with exit code 124 and each live rank's last
+    collectives on stderr, well inside the driver's limit -- not a silent hang."""
+    env = _env()
+    env["NXD_FAULT_INJECT"] = "bench_microstep@1#2:hang"
+    env["NXD_BENCH_WATCHDOG_S"] = "20"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 124, (r.returncode, r.stderr[-3000:])
+    assert "step watchdog: no progress" in r.stderr
+    assert "last collectives issued" in r.stderr and "#" in r.stderr.split("last collectives issued")[1]
+    assert not _json_lines(r.stdout)

@@ -1,0 +1,102 @@
+"""TP=2 serving on the GPU kernels (the fork's notebook config: Llama-3.2-1B, tp_degree=2; reference
+examples/inference/llama3_2_inference.ipynb cell 8, trace/spmd.py:82-187), rehearsed on the one
+MI355X of the test box: SpmdGenerationServer with 2 resident worker ranks sharing cuda:0 over gloo
+(host-staged collectives, so decode runs eagerly), against a TP=1 server on the same GPU (RCCL
+world of 1, hipGraph decode through the fused kernels).
+
+bf16 TP=2 and TP=1 round their partial sums differently (the row-parallel all-reduce adds two bf16
+partials), so a random-init model can flip a greedy argmax where its top-2 logits nearly tie.  The
+check: greedy tokens identical for all 64 new tokens -- or, at the first differing position,
+teacher-forced prefill logits of both servers agree (relative max error <= 2e-2) and the TP=1
+top-2 margin there is within the measured TP=1 / TP=2 logit difference (a genuine near-tie).  The
+"peaked" model (untied lm_head = a row permutation of the embedding: next token = pi(current) by a
+wide margin) must match exactly."""
+
+import os
+import tempfile
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(kind):
+    from transformers import LlamaConfig
+
+    if kind == "tiny":
+        d = dict(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+                 num_key_value_heads=2, vocab_size=2048, tie_word_embeddings=True)
+    else:   # Llama-3.2-1B geometry
+        d = dict(hidden_size=2048, intermediate_size=8192, num_hidden_layers=16, num_attention_heads=32,
+                 num_key_value_heads=8, vocab_size=128256, tie_word_embeddings=kind != "peaked")
+    d.update(max_position_embeddings=2048, rms_norm_eps=1e-5, rope_theta=500000.0, bos_token_id=1, eos_token_id=2,
+             rope_scaling={"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                           "original_max_position_embeddings": 8192})
+    return LlamaConfig(**d)
+
+
+def _random_full_state(cfg, kind, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    H, I, V = cfg.hidden_size, cfg.intermediate_size, cfg.vocab_size
+    nq, nkv = cfg.num_attention_heads, cfg.num_key_value_heads
+    D = H // nq
+
+    def rnd(*shape, std=0.02):
+        return (torch.randn(*shape, generator=g, device="cuda") * std).to(torch.bfloat16).cpu()
+
+    emb_std = 1.0 if kind == "peaked" else 0.05
+    sd = {"model.embed_tokens.weight": rnd(V, H, std=emb_std), "model.norm.weight": torch.ones(H, dtype=torch.bfloat16)}
+    for i in range(cfg.num_hidden_layers):
+        p = f"model.layers.{i}."
+        sd[p + "self_attn.qkv_proj.weight_qkv"] = rnd((nq + 2 * nkv) * D, H)
+        sd[p + "self_attn.o_proj.weight"] = rnd(H, nq * D, std=0.02 / (2 * cfg.num_hidden_layers) ** 0.5)
+        sd[p + "mlp.gate_up_proj.weight"] = rnd(2 * I, H)
+        sd[p + "mlp.down_proj.weight"] = rnd(H, I, std=0.02 / (2 * cfg.num_hidden_layers) ** 0.5)
+        sd[p + "input_layernorm.weight"] = torch.ones(H, dtype=torch.bfloat16)
+        sd[p + "post_attention_layernorm.weight"] = torch.ones(H, dtype=torch.bfloat16)
+    if kind == "peaked":
+        perm = torch.randperm(V, generator=torch.Generator().manual_seed(seed + 1))
+        sd["lm_head.weight"] = sd["model.embed_tokens.weight"][torch.argsort(perm)].contiguous()
+    else:
+        sd["lm_head.weight"] = sd["model.embed_tokens.weight"]
+    return sd
+
+
+@pytest.mark.parametrize("kind", ["tiny", "llama3.2-1b", "peaked"])
+def test_tp2_server_greedy_matches_tp1_on_gpu(kind):
+    from neuronx_distributed_llama3_2_amd.inference.spmd_server import SpmdGenerationServer
+
+    cfg = _cfg(kind)
+    d = tempfile.mkdtemp()
+    path = os.path.join(d, "full.pt")
+    torch.save(_random_full_state(cfg, kind), path)
+    torch.manual_seed(5)
+    ids = torch.randint(3, cfg.vocab_size, (2, 16))
+    kw = dict(batch_size=2, seq_len=128, max_context_length=96)
+    new = 64
+    outs, servers = {}, {}
+    try:
+        for tp in (1, 2):
+            servers[tp] = SpmdGenerationServer.from_full_state_dict(cfg.to_dict(), path, tp, kw, dtype="bfloat16")
+            outs[tp] = servers[tp].generate(ids, max_new_tokens=new, eos_token_id=-1)
+        a, b = outs[1], outs[2]
+        assert a.shape == b.shape == (2, 16 + new)
+        if kind == "peaked" or torch.equal(a, b):
+            assert torch.equal(a, b), (a, b)
+            return
+        # first differing position: teacher-forced logits of both servers on TP=1's prefix
+        diff = (a != b).any(0).nonzero()[0].item()
+        assert diff >= 16
+        prefix = a[:, :diff]
+        la = servers[1].pool.call("_context_encode", prefix).float()
+        lb = servers[2].pool.call("_context_encode", prefix).float()
+        err = (la - lb).abs().max() / la.abs().max()
+        assert err <= 2e-2, float(err)
+        top2 = la.topk(2, dim=-1).values
+        margin = (top2[:, 0] - top2[:, 1]).min()
+        assert margin <= 2 * (la - lb).abs().max(), (diff, float(margin), float((la - lb).abs().max()))
+        print(f"{kind}: identical for {diff - 16} new tokens, then a near-tie (margin {float(margin):.4f})")
+    finally:
+        for s in servers.values():
+            s.close()

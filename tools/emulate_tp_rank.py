@@ -178,6 +178,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-sp", action="store_true")
+    ap.add_argument("--ckpt", default=None, choices=[None, "selective", "full"], help="activation checkpointing")
     ap.add_argument("--cpu", action="store_true", help="plumbing check on the CPU (tiny models)")
     ap.add_argument("--hidden", type=int, default=None, help="(CPU plumbing) override hidden size")
     ap.add_argument("--link-gbps", type=float, default=None,
@@ -218,6 +219,10 @@ def main():
     over = dict(sequence_parallel_enabled=(a.tp > 1 and not a.no_sp), max_position_embeddings=max(8192, a.seq))
     if a.layers is not None:
         over["num_hidden_layers"] = a.layers
+    if a.ckpt == "full":
+        over["activation_checkpoint"] = "full"
+    elif a.ckpt == "selective":
+        over["selective_checkpoint_enabled"] = True
     if a.hidden is not None:
         over.update(hidden_size=a.hidden, intermediate_size=4 * a.hidden, vocab_size=1024 * a.tp)
     cfg = llama_config(a.model, **over)
@@ -277,6 +282,14 @@ def main():
            "node_tokens_per_s_comm_free": round(a.gbs * a.seq / el, 1),
            "params_per_rank": sum(p.numel() for p in model.parameters()),
            "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if use_cuda else 0.0, **mem}
+    if use_cuda:
+        from neuronx_distributed_llama3_2_amd.utils.memory_planner import plan_training_memory
+
+        plan = plan_training_memory(cfg, tp=a.tp, mbs=mbs, seq=a.seq, sequence_parallel=over["sequence_parallel_enabled"],
+                                    activation_checkpoint=a.ckpt, zero1=False)
+        rec["ckpt"] = a.ckpt
+        rec["planner_gib"] = round(plan.total_bytes / 2**30, 1)
+        rec["planner_err_pct"] = round(100 * (plan.total_bytes / 2**30 - rec["peak_mem_gib"]) / rec["peak_mem_gib"], 1)
     print(json.dumps(rec), flush=True)
     dist.destroy_process_group()
 
