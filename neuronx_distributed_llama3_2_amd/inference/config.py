@@ -58,6 +58,8 @@ class InferenceConfig:
         self.temperature = kwargs.pop("temperature", 1.0)
         self.num_beams = kwargs.pop("num_beams", 1)
         self.use_hip_graphs = kwargs.pop("use_hip_graphs", True)
+        # bitwise-reproducible decode: no fp32-atomic fused attention + o_proj launch (model_base.py)
+        self.deterministic = kwargs.pop("deterministic", False)
         # context encoding captured per (batch, bucket) hipGraph as well (needs use_hip_graphs)
         self.prefill_graphs = kwargs.pop("prefill_graphs", True)
         # GQA sharding (modules/gqa.py): "replicate-to-tp-degree" (default) | "convert-to-mha"

@@ -176,6 +176,8 @@ class LlamaForCausalLMInference:
                 self.model_config = model_config
         self.model = self._model_cls(model_config, dtype=dtype,
                                      device=torch.device("meta") if not init_weights else self.device)
+        # InferenceConfig(deterministic=True): no fp32-atomic fused decode launches (model_base.py)
+        self.model._decode_deterministic = bool(getattr(config, "deterministic", False))
         if config.quantized:
             self._quantize()
         self.max_batch = config.max_batch_size

@@ -39,7 +39,10 @@ from ..parallel_layers.parallel_state import get_tensor_model_parallel_size
 _PREFETCH_MB = float(os.environ.get("NXD_DECODE_PREFETCH_MB", "0"))
 _PREFETCH_WGS = int(os.environ.get("NXD_DECODE_PREFETCH_WGS", "256"))
 # decode attention + o_proj in one launch (csrc/decode_attn.hip FUSE); the o_proj sum reaches the
-# residual stream through the next two fused GEMVs (xadd / yadd side inputs)
+# residual stream through the next two fused GEMVs (xadd / yadd side inputs).  Its rows are summed
+# with fp32 atomics, so the low bits of a token's logits -- and rarely a greedy near-tie -- can vary
+# from run to run; InferenceConfig(deterministic=True) or NXD_DECODE_ATTN_OPROJ=0 takes the
+# two-launch path (bitwise-reproducible decode, ~5 % slower per token).
 _ATTN_OPROJ = os.environ.get("NXD_DECODE_ATTN_OPROJ", "1") == "1"
 
 
@@ -202,7 +205,8 @@ class DecoderInferenceMixin:
                 # spare workgroups of the attention launch pull o_proj and the head of gate_up into
                 # the Infinity Cache while the (latency-bound) attention leaves HBM idle
                 C.decode_attn_prefetch(attn.o_proj.weight, -1, w_gu, int(_PREFETCH_MB * 2**20), _PREFETCH_WGS)
-            oacc = self._decode_oacc(M, res) if (_ATTN_OPROJ and _PREFETCH_MB <= 0) else None
+            fuse_o = _ATTN_OPROJ and _PREFETCH_MB <= 0 and not getattr(self, "_decode_deterministic", False)
+            oacc = self._decode_oacc(M, res) if fuse_o else None
             if oacc is not None and C.decode_attn_oproj(q, kc, vc, sid32, cache_len.to(torch.int32), attn.o_proj.weight,
                                                         oacc, 1.0 / math.sqrt(D)):
                 # oacc += o_proj(attention) (one launch); the GLU prologue sees res + oacc, the down
