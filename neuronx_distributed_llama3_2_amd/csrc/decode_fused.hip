@@ -56,6 +56,10 @@ struct Params {
   int pf;                 // issue the epilogue's / prologue's own global reads (residual row, yadd,
                           // position + cos/sin, RMSNorm weight) at kernel start, next to the first
                           // weight round, instead of as dependent round trips after the GEMV
+  int nt;                 // weight rows loaded non-temporal (global_load ... nt): decode reads every
+                          // weight byte once per token (MI355X_MICROARCH.md, nt-weights).  Llama-3.2-1B
+                          // bs=1: 0.732 -> 0.712 ms/token, alternating A/B on one box
+                          // (profiles/r4_decode_nt_fn_ab.txt)
 };
 
 constexpr int U = 4;   // 512-element k-steps per load round
@@ -108,12 +112,23 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
   const int kbeg = min(ks * kc, p.K), kend = min(p.K, kbeg + kc);
   u32x4_t wv[NW][U];
   auto load_round = [&](int base) {
+    if (p.nt) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = base + lane * 8 + u * 512;
+      for (int u = 0; u < U; ++u) {
+        const int k = base + lane * 8 + u * 512;
 #pragma unroll
-      for (int r = 0; r < NW; ++r)
-        wv[r][u] = k < kend ? *reinterpret_cast<const u32x4_t*>(p.w + (int64_t)rows[r] * p.ldw + k) : u32x4_t{0, 0, 0, 0};
+        for (int r = 0; r < NW; ++r)
+          wv[r][u] = k < kend ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p.w + (int64_t)rows[r] * p.ldw + k))
+                              : u32x4_t{0, 0, 0, 0};
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = base + lane * 8 + u * 512;
+#pragma unroll
+        for (int r = 0; r < NW; ++r)
+          wv[r][u] = k < kend ? *reinterpret_cast<const u32x4_t*>(p.w + (int64_t)rows[r] * p.ldw + k) : u32x4_t{0, 0, 0, 0};
+      }
     }
   };
   load_round(kbeg);
@@ -321,6 +336,7 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
 int g_glu_pairs = 1;   // knob 0: (gate, up) row pairs per wave of the GLU projection (1 | 2)
 int g_ks = 0;          // knob 1: k-slices per row group (0 = pick_ks)
 int g_pf = -1;         // knob 2: early epilogue / prologue reads (Params::pf; NXD_DECODE_EPI_PF, default 1)
+int g_nt = -1;         // knob 3: non-temporal weight loads (Params::nt; NXD_DECODE_NT, default 1)
 
 static int pick_ks(int groups, int K) {
   if (g_ks == 1 || g_ks == 2 || g_ks == 4) return g_ks;
@@ -374,6 +390,7 @@ void dgemv_set_knob(int which, int value) {
   if (which == 0) dfused::g_glu_pairs = value == 2 ? 2 : 1;
   else if (which == 1) dfused::g_ks = value;
   else if (which == 2) dfused::g_pf = value != 0;
+  else if (which == 3) dfused::g_nt = value != 0;
 }
 
 int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,
@@ -386,12 +403,17 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
   dfused::Params p{static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(norm_w), eps,
                    static_cast<const uint16_t*>(w), ldw, static_cast<uint16_t*>(y), ldy, M, N, K, nq, nkv, D, cos_t,
                    sin_t, pos, T, static_cast<uint16_t*>(kc), static_cast<uint16_t*>(vc), c_sb, c_sh, c_sl, cache_idx,
-                   Lmax, max_pos, xadd, yadd, 1};
+                   Lmax, max_pos, xadd, yadd, 1, 1};
   if (dfused::g_pf < 0) {
     const char* e = getenv("NXD_DECODE_EPI_PF");
     dfused::g_pf = e ? (atoi(e) != 0) : 1;
   }
   p.pf = dfused::g_pf;
+  if (dfused::g_nt < 0) {
+    const char* e = getenv("NXD_DECODE_NT");
+    dfused::g_nt = e ? (atoi(e) != 0) : 1;
+  }
+  p.nt = dfused::g_nt;
   const bool norm = norm_w != nullptr;
   if (M == 1) return dfused::dispatch<1>(p, epi, norm, stream);
   if (M == 2) return dfused::dispatch<2>(p, epi, norm, stream);
