@@ -294,7 +294,14 @@ class LlamaForCausalLM(nn.Module):
 
     def _forward_interleaved(self, input_ids, attention_mask, labels) -> CausalLMOutput:
         """Training forward of TP + SP as two half micro-batches on two streams, their collectives
-        interleaved (parallel_layers/stream_split.py); same loss as the one-pass forward."""
+        interleaved (parallel_layers/stream_split.py); same loss as the one-pass forward.
+
+        Returns logits=None: the halves' logits are two buffers that the fused cross-entropy
+        backward overwrites in place (inplace_backward), and joining them would copy the whole
+        vocab-parallel logits (~2 GiB per micro-batch at TP=8) only to be clobbered.  A caller that
+        needs training logits runs with NXD_SP_STREAMS=1 (the one-pass path); that path is also the
+        one that runs forward hooks registered on the decoder layers (this one calls
+        `LlamaDecoderLayer.forward_stages`, not `forward`)."""
         h = input_ids.shape[0] // 2
         am = (attention_mask[:h], attention_mask[h:]) if attention_mask is not None else (None, None)
         self.model.rope_cache.tables(input_ids.device)   # built once on this stream, read by both halves
