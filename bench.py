@@ -334,7 +334,7 @@ def main(a):
             # caching-allocator events inside the timed steps (a retry = OOM -> free cache -> device sync)
             "num_alloc_retries": int(ms1.get("num_alloc_retries", 0) - ms0.get("num_alloc_retries", 0)),
             "rccl_max_channels": os.environ.get("NCCL_MAX_NCHANNELS", "rccl default"),
-            "sp_streams": 2 if stream_split.enabled() and over["sequence_parallel_enabled"] else 1,
+            "sp_streams": stream_split.parts() if over["sequence_parallel_enabled"] else 1,
             "api": "nxd.initialize_parallel_model / initialize_parallel_optimizer",
         }
         print(json.dumps(rec), flush=True)

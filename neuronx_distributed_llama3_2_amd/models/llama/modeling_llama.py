@@ -251,8 +251,9 @@ class LlamaForCausalLM(nn.Module):
 
     def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                 labels: Optional[torch.Tensor] = None, position_ids=None, **unused) -> CausalLMOutput:
-        if self._interleave(input_ids, labels):
-            return self._forward_interleaved(input_ids, attention_mask, labels)
+        k = self._interleave(input_ids, labels)
+        if k:
+            return self._forward_interleaved(input_ids, attention_mask, labels, k)
         hidden = self.model(input_ids)
         logits = self.lm_head(hidden)  # [S, B, V/tp]
         loss = None
@@ -272,16 +273,22 @@ class LlamaForCausalLM(nn.Module):
         per_tok = parallel_cross_entropy(logits, shifted, inplace_backward=True)
         return per_tok.sum(), (shifted != -100).sum().clamp(min=1)
 
-    def _interleave(self, input_ids, labels) -> bool:
+    def _interleave(self, input_ids, labels) -> int:
+        """Parts of the micro-batch for the interleaved forward (0 = one pass)."""
         m = self.model
         if isinstance(input_ids, torch.fx.Proxy) or torch.fx._symbolic_trace.is_fx_tracing():
-            return False   # pipeline partitioning traces the one-pass forward
-        return (stream_split.enabled() and self.training and torch.is_grad_enabled() and labels is not None
+            return 0   # pipeline partitioning traces the one-pass forward
+        if not (stream_split.enabled() and self.training and torch.is_grad_enabled() and labels is not None
                 and get_pipeline_model_parallel_size() == 1
                 and m.sequence_parallel_enabled and m.activation_checkpoint != "full"
-                and input_ids.dim() == 2 and input_ids.shape[0] % 2 == 0 and get_data_parallel_size() == 1)
+                and input_ids.dim() == 2 and get_data_parallel_size() == 1):
+            return 0
+        k = min(stream_split.parts(), input_ids.shape[0])
+        while k > 1 and input_ids.shape[0] % k:
+            k -= 1
+        return k if k >= 2 else 0
 
-    def _half(self, ids, labels, attention_mask):
+    def _part(self, ids, labels, attention_mask):
         m = self.model
         hidden = m.embed_tokens(ids.t().contiguous())
         residual = None
@@ -292,25 +299,27 @@ class LlamaForCausalLM(nn.Module):
         yield
         return self._loss_terms(logits, labels, attention_mask)
 
-    def _forward_interleaved(self, input_ids, attention_mask, labels) -> CausalLMOutput:
-        """Training forward of TP + SP as two half micro-batches on two streams, their collectives
+    def _forward_interleaved(self, input_ids, attention_mask, labels, k: int = 2) -> CausalLMOutput:
+        """Training forward of TP + SP as k parts of the micro-batch on k streams, their collectives
         interleaved (parallel_layers/stream_split.py); same loss as the one-pass forward.
 
-        Returns logits=None: the halves' logits are two buffers that the fused cross-entropy
+        Returns logits=None: the parts' logits are separate buffers that the fused cross-entropy
         backward overwrites in place (inplace_backward), and joining them would copy the whole
         vocab-parallel logits (~2 GiB per micro-batch at TP=8) only to be clobbered.  A caller that
         needs training logits runs with NXD_SP_STREAMS=1 (the one-pass path); that path is also the
         one that runs forward hooks registered on the decoder layers (this one calls
         `LlamaDecoderLayer.forward_stages`, not `forward`)."""
-        h = input_ids.shape[0] // 2
-        am = (attention_mask[:h], attention_mask[h:]) if attention_mask is not None else (None, None)
-        self.model.rope_cache.tables(input_ids.device)   # built once on this stream, read by both halves
-        gens = [self._half(input_ids[:h], labels[:h], am[0]), self._half(input_ids[h:], labels[h:], am[1])]
-        (s0, n0), (s1, n1) = stream_split.run_interleaved(gens, input_ids.device)
+        n = input_ids.shape[0] // k
+        sl = [slice(i * n, (i + 1) * n) for i in range(k)]
+        self.model.rope_cache.tables(input_ids.device)   # built once on this stream, read by every part
+        gens = [self._part(input_ids[s], labels[s], attention_mask[s] if attention_mask is not None else None)
+                for s in sl]
+        terms = stream_split.run_interleaved(gens, input_ids.device)
         if input_ids.is_cuda:
-            for t in (s0, n0, s1, n1):   # made on the halves' streams, read on this one
-                t.record_stream(torch.cuda.current_stream())
-        loss = (s0 + s1) / (n0 + n1)
+            for pair in terms:   # made on the parts' streams, read on this one
+                for t in pair:
+                    t.record_stream(torch.cuda.current_stream())
+        loss = sum(t[0] for t in terms) / sum(t[1] for t in terms)
         return CausalLMOutput(loss=loss, logits=None)
 
 

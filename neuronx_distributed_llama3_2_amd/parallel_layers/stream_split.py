@@ -23,7 +23,8 @@ Shared state the two streams write is serialised here:
 
 Active only while training with TP > 1, sequence parallelism, DP = 1 (the backward-overlapped DP
 bucket reduction counts one gradient report per parameter) and no full activation checkpointing;
-NXD_SP_STREAMS=2 turns it on; off (1) by default until it has run on a multi-GPU node.  Checked:
+NXD_SP_STREAMS=k (k >= 2) turns it on with k parts of the micro-batch on k streams (the largest
+divisor of the micro-batch <= k); off (1) by default until it has run on a multi-GPU node.  Checked:
 fp32 CPU parity with the one-pass step (tests/test_stream_split.py, TP=2 and TP=4 replicated kv);
 on the GPU kernels (one-GPU gloo rehearsal, TP=4 replicated kv, 4 AdamW steps, three runs each)
 bit-identical from run to run and within 3e-4 of the one-pass losses / grad norms
@@ -44,25 +45,37 @@ _active = False           # inside an interleaved forward/backward (set until jo
 _streams = {}             # device index -> [stream A, stream B]
 
 
+def parts() -> int:
+    """Streams (micro-batch parts) requested: 1 = off."""
+    try:
+        return max(1, int(_MODE))
+    except ValueError:
+        return 1
+
+
 def enabled() -> bool:
-    return _MODE == "2"
+    return parts() >= 2
 
 
-def set_enabled(on: bool) -> None:
+def set_enabled(on, n: int = None) -> None:
+    """set_enabled(True) -> 2 parts; set_enabled(True, n) or set_enabled(n) -> n parts; False -> off."""
     global _MODE
-    _MODE = "2" if on else "1"
+    if n is None and not isinstance(on, bool):
+        n = int(on)
+    k = (n if n is not None else 2) if on else 1
+    _MODE = str(max(1, int(k)))
 
 
 def active() -> bool:
     return _active
 
 
-def streams_for(device: torch.device) -> List[torch.cuda.Stream]:
+def streams_for(device: torch.device, n: int = 2) -> List[torch.cuda.Stream]:
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    s = _streams.get(idx)
-    if s is None:
-        s = _streams[idx] = [torch.cuda.Stream(device=idx), torch.cuda.Stream(device=idx)]
-    return s
+    s = _streams.setdefault(idx, [])
+    while len(s) < n:
+        s.append(torch.cuda.Stream(device=idx))
+    return s[:n]
 
 
 def run_interleaved(gens: Sequence[Generator], device: torch.device) -> list:
@@ -74,7 +87,7 @@ def run_interleaved(gens: Sequence[Generator], device: torch.device) -> list:
     cuda = device.type == "cuda"
     if cuda:
         main = torch.cuda.current_stream(device)
-        ss = streams_for(device)
+        ss = streams_for(device, len(gens))
         for s in ss:
             s.wait_stream(main)   # weights / zeroed grads / inputs written on the caller's stream
         _active = True

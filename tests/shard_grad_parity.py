@@ -30,7 +30,7 @@ def _w_grads(rank, world, preset, sp, streams, dev_kind, out):
         torch.cuda.set_device(0)
     dev = torch.device(dev_kind)
     dtype = torch.bfloat16 if dev_kind == "cuda" else torch.float32
-    stream_split.set_enabled(streams == 2)
+    stream_split.set_enabled(streams >= 2, streams)
     ps.initialize_model_parallel(world)
     seq = 512 if dev_kind == "cuda" else 128
     cfg = llama_config(preset, sequence_parallel_enabled=sp, max_position_embeddings=seq)

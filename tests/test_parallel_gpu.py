@@ -31,7 +31,7 @@ def _w_train(rank, world, preset, sp, out, streams=1):
     from neuronx_distributed_llama3_2_amd.parallel_layers import stream_split
 
     # streams=2: the two-stream SP half micro-batch interleaving (NXD_SP_STREAMS=2, opt-in)
-    stream_split.set_enabled(streams == 2)
+    stream_split.set_enabled(streams >= 2, streams)
     from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
     from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW
     from neuronx_distributed_llama3_2_amd.parallel.grad_buffer import find_shared_params

@@ -17,7 +17,7 @@ def _w(rank, world, streams, out, preset="tiny8"):
     from neuronx_distributed_llama3_2_amd.parallel_layers import parallel_state as ps
     from neuronx_distributed_llama3_2_amd.parallel_layers import stream_split
 
-    stream_split.set_enabled(streams == 2)
+    stream_split.set_enabled(streams >= 2, streams)
     ps.initialize_model_parallel(world)
     cfg = llama_config(preset, sequence_parallel_enabled=True, max_position_embeddings=128, num_hidden_layers=2)
     torch.manual_seed(0)
@@ -65,6 +65,15 @@ def test_interleaved_halves_match_one_pass_tp2():
 def test_interleaved_halves_match_one_pass_tp4_replicated_kv():
     # tiny: 2 kv heads at TP=4 -> kv heads replicated on 2 ranks (KV-group all-reduce in backward)
     a, b = _run(4, 1, "tiny"), _run(4, 2, "tiny")
+    assert b["interleaved"] == 3
+    for i in range(3):
+        assert abs(a["loss"][i] - b["loss"][i]) < 1e-4 * abs(a["loss"][i]), (a, b)
+        assert abs(a["gn"][i] - b["gn"][i]) < 1e-3 * a["gn"][i], (a, b)
+
+
+def test_four_parts_match_one_pass_tp2():
+    # NXD_SP_STREAMS=4: the micro-batch of 4 as four parts on four streams
+    a, b = _run(2, 1), _run(2, 4)
     assert b["interleaved"] == 3
     for i in range(3):
         assert abs(a["loss"][i] - b["loss"][i]) < 1e-4 * abs(a["loss"][i]), (a, b)

@@ -188,7 +188,7 @@ def main():
                     help="collective buffer lifetime: stash until wait() (RCCL default) or record_stream")
     ap.add_argument("--spin", choices=["realtime", "sleep"], default="realtime",
                     help="link spin: real-time-counter copy kernel, or round-3's torch.cuda._sleep")
-    ap.add_argument("--sp-streams", type=int, default=None, help="NXD_SP_STREAMS for this run (1 or 2)")
+    ap.add_argument("--sp-streams", type=int, default=None, help="NXD_SP_STREAMS for this run (1 = one pass, k >= 2 parts)")
     a = ap.parse_args()
 
     from torch.testing._internal.distributed.fake_pg import FakeStore
@@ -211,7 +211,7 @@ def main():
     if a.sp_streams is not None:
         from neuronx_distributed_llama3_2_amd.parallel_layers import stream_split
 
-        stream_split.set_enabled(a.sp_streams == 2)
+        stream_split.set_enabled(a.sp_streams >= 2, a.sp_streams)
     if a.link_gbps and use_cuda:
         _LINK = _Link(a.link_gbps, a.link_cus, a.spin)
     ps.initialize_model_parallel(tensor_model_parallel_size=a.tp)
@@ -274,9 +274,9 @@ def main():
            "layers": cfg.num_hidden_layers, "seq": a.seq, "mbs": mbs, "gbs": a.gbs, "grad_accum": accum,
            "sp_chunks": __import__("neuronx_distributed_llama3_2_amd.parallel_layers.sp", fromlist=["x"])
            .get_sequence_parallel_chunks(a.tp), "link_gbps": a.link_gbps,
-           "link_cus": a.link_cus if _LINK else None, "spin": a.spin if _LINK else None, "sync": a.sync,
-           "sp_streams": 2 if __import__("neuronx_distributed_llama3_2_amd.parallel_layers.stream_split",
-                                          fromlist=["x"]).enabled() else 1,
+           "link_cus": a.link_cus if _LINK else None, "gemm_no_streamk": os.environ.get("NXD_GEMM_NO_STREAMK", "0"), "spin": a.spin if _LINK else None, "sync": a.sync,
+           "sp_streams": __import__("neuronx_distributed_llama3_2_amd.parallel_layers.stream_split",
+                                     fromlist=["x"]).parts(),
            "link_busy_ms_per_step": round(1000 * _LINK.busy_s / (a.warmup + a.steps), 2) if _LINK else None,
            "ms_per_step": round(1000 * el, 2), "ms_per_microbatch": round(1000 * el / accum, 2),
            "node_tokens_per_s_comm_free": round(a.gbs * a.seq / el, 1),

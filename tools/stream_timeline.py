@@ -2,9 +2,10 @@
 the link model: the link is the `cu_stream_kernel` spin on its own stream).
 
 For the last optimizer step (between the last two AdamW launch groups) it reports wall time and
-the union-of-intervals time of: compute kernels (any stream), link spins, both at once, neither
-(GPU idle), and compute-idle-while-link-busy (exposed link time), split into the forward half
-(up to the first flash-attention backward launch) and the backward + optimizer half.
+the union-of-intervals time of: compute kernels (every stream but the link's), link work (the spin
+and the receiving-side copies on the link stream), both at once, neither (GPU idle), and
+compute-idle-while-link-busy (exposed link time), split into the forward half (up to the first
+flash-attention backward launch) and the backward + optimizer half.
 
     python tools/stream_timeline.py gpurun_out/<dir>/run_kernel_trace.csv [--json]
 """
@@ -64,8 +65,10 @@ def main(path, as_json=False):
     end = groups[-1][-1] + 1
     sel = rows[start:end]
     t0, t1 = sel[0][0], max(r[1] for r in sel)
-    link = union([[s, e] for s, e, n, q in sel if "cu_stream_kernel" in n])
-    comp = union([[s, e] for s, e, n, q in sel if "cu_stream_kernel" not in n])
+    # link work = everything on the link model's stream (the spin and the receiving-side copies)
+    lq = {q for s, e, n, q in sel if "cu_stream_kernel" in n}
+    link = union([[s, e] for s, e, n, q in sel if q in lq])
+    comp = union([[s, e] for s, e, n, q in sel if q not in lq])
     fab = [s for s, e, n, q in sel if "fab::" in n]
     tb = min(fab) if fab else t1
     res = {"trace": path, "kernels": len(sel), "streams": sorted({q for *_, q in sel})}
