@@ -338,8 +338,20 @@ int g_ks = 0;          // knob 1: k-slices per row group (0 = pick_ks)
 int g_pf = -1;         // knob 2: early epilogue / prologue reads (Params::pf; NXD_DECODE_EPI_PF, default 1)
 int g_nt = -1;         // knob 3: non-temporal weight loads (Params::nt; NXD_DECODE_NT, default 1)
 
-static int pick_ks(int groups, int K) {
+// per-projection override (A/B): NXD_DECODE_KS_PLAIN / _RESID / _GLU / _QKV = 1 | 2 | 4
+static int g_ks_epi[4] = {-2, -2, -2, -2};
+
+static int pick_ks(int groups, int K, int epi) {
   if (g_ks == 1 || g_ks == 2 || g_ks == 4) return g_ks;
+  if (g_ks_epi[0] == -2) {
+    const char* names[4] = {"NXD_DECODE_KS_PLAIN", "NXD_DECODE_KS_RESID", "NXD_DECODE_KS_GLU", "NXD_DECODE_KS_QKV"};
+    for (int i = 0; i < 4; ++i) {
+      const char* e = getenv(names[i]);
+      g_ks_epi[i] = e ? atoi(e) : 0;
+    }
+  }
+  const int f = g_ks_epi[epi & 3];
+  if (f == 1 || f == 2 || f == 4) return f;
   int ks = 1;
   while (ks < 4 && groups * ks * 2 <= 8192 && K / (ks * 2) >= 1024) ks *= 2;
   return ks;
@@ -348,7 +360,7 @@ static int pick_ks(int groups, int K) {
 template <int MM, int NW, int EPI, bool NORM>
 static int launch(const Params& p, int groups, hipStream_t s) {
   const size_t lds = NORM ? (size_t)MM * p.K * 2 : 0;
-  const int ks = pick_ks(groups, p.K);
+  const int ks = pick_ks(groups, p.K, EPI);
   const dim3 grid((unsigned)((groups * ks + 3) / 4)), block(256);
   if (ks == 4)
     hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 4>), grid, block, lds, s, p);
