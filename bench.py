@@ -190,7 +190,7 @@ def main(a):
     backend = "nccl" if use_cuda and not a.gloo_gpu else "gloo"
     from neuronx_distributed_llama3_2_amd.parallel.rccl_env import apply_rccl_env
 
-    apply_rccl_env()
+    apply_rccl_env(world_size=world)
     # a failed / timed-out RCCL collective tears the process down (TORCH_NCCL_ASYNC_ERROR_HANDLING)
     # instead of hanging every rank; the host watchdog below catches what that does not
     wd_s = float(os.environ.get("NXD_BENCH_WATCHDOG_S", "300"))
@@ -334,6 +334,7 @@ def main(a):
             # caching-allocator events inside the timed steps (a retry = OOM -> free cache -> device sync)
             "num_alloc_retries": int(ms1.get("num_alloc_retries", 0) - ms0.get("num_alloc_retries", 0)),
             "rccl_max_channels": os.environ.get("NCCL_MAX_NCHANNELS", "rccl default"),
+            "streamk_max_cus": os.environ.get("TENSILE_STREAMK_MAX_CUS", "all"),
             "sp_streams": stream_split.parts() if over["sequence_parallel_enabled"] else 1,
             "api": "nxd.initialize_parallel_model / initialize_parallel_optimizer",
         }

@@ -42,17 +42,27 @@ RCCL_DEFAULTS: Dict[str, str] = {
 
 DEFAULT_CHANNELS = 16
 
-_PREFIXES = ("NCCL_", "RCCL_", "TORCH_NCCL_", "NXD_RCCL", "NXD_COMM", "NXD_SP_CHUNKS", "HSA_ENABLE_IPC")
+_PREFIXES = ("NCCL_", "RCCL_", "TORCH_NCCL_", "NXD_RCCL", "NXD_COMM", "NXD_SP_CHUNKS", "HSA_ENABLE_IPC",
+             "TENSILE_STREAMK")
 _logged = False
 
 
-def apply_rccl_env(extra: Optional[Dict[str, str]] = None) -> Dict[str, str]:
+def apply_rccl_env(extra: Optional[Dict[str, str]] = None, world_size: int = 1) -> Dict[str, str]:
     """Set the library's RCCL defaults (and `extra`) where the environment does not already
-    define them.  Returns what was set.  Call before `torch.distributed.init_process_group`."""
+    define them.  Returns what was set.  Call before `torch.distributed.init_process_group`.
+
+    NXD_COMM_RESERVE_CUS=n (multi-rank runs only): cap hipBLASLt's persistent stream-K GEMMs at
+    (CUs - n) workgroups (TENSILE_STREAMK_MAX_CUS), so n CUs stay free for the RCCL channel
+    kernels: a stream-K GEMM holds one workgroup on every CU for its whole duration, and a
+    collective launched behind it cannot start until one retires (the emulated TP=8 rank's link
+    kernels started late behind them: profiles/r4_stream_timeline_8layers.jsonl)."""
     want = dict(RCCL_DEFAULTS)
     ch = os.environ.get("NXD_RCCL_CHANNELS", str(DEFAULT_CHANNELS))
     if ch and ch not in ("0", "auto"):
         want["NCCL_MAX_NCHANNELS"] = ch
+    reserve = int(os.environ.get("NXD_COMM_RESERVE_CUS", "0") or 0)
+    if reserve > 0 and world_size > 1:
+        want["TENSILE_STREAMK_MAX_CUS"] = str(max(1, _num_cus() - reserve))
     if extra:
         want.update(extra)
     applied = {}
@@ -61,6 +71,17 @@ def apply_rccl_env(extra: Optional[Dict[str, str]] = None) -> Dict[str, str]:
             os.environ[k] = str(v)
             applied[k] = str(v)
     return applied
+
+
+def _num_cus() -> int:
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            return int(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
+    except Exception:  # pragma: no cover
+        pass
+    return 256
 
 
 def comm_config() -> Dict[str, str]:

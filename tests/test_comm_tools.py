@@ -54,3 +54,16 @@ def test_default_channel_cap_logged(monkeypatch):
     monkeypatch.delenv("NXD_RCCL_CHANNELS")
     rccl_env.apply_rccl_env()
     assert os.environ["NCCL_MAX_NCHANNELS"] == "40"
+
+
+def test_comm_cu_reservation_only_for_multi_rank(monkeypatch):
+    from neuronx_distributed_llama3_2_amd.parallel import rccl_env
+
+    monkeypatch.delenv("TENSILE_STREAMK_MAX_CUS", raising=False)
+    monkeypatch.setenv("NXD_COMM_RESERVE_CUS", "16")
+    monkeypatch.setattr(rccl_env, "_num_cus", lambda: 256)
+    applied = rccl_env.apply_rccl_env(world_size=1)
+    assert "TENSILE_STREAMK_MAX_CUS" not in applied
+    applied = rccl_env.apply_rccl_env(world_size=8)
+    assert applied["TENSILE_STREAMK_MAX_CUS"] == "240"
+    monkeypatch.delenv("TENSILE_STREAMK_MAX_CUS", raising=False)
