@@ -5,7 +5,7 @@ set -o pipefail
 O=gpurun_out/r4skcus; mkdir -p $O
 export TMPDIR=/tmp
 E="python -u tools/emulate_tp_rank.py --steps 3 --warmup 1 --tp 8 --link-gbps 400 --sp-streams 2"
-run() { echo "== $*" >&2; timeout -k 10 300 $E "$@" 2>> $O/emulate.err | grep '^{' | sed "s/^{/{\"streamk_max_cus\": \"${TENSILE_STREAMK_MAX_CUS:-all}\", /" >> $O/emulate.jsonl || exit $?; }
+run() { echo "== $*" >&2; timeout -k 10 300 $E "$@" > $O/run.log 2>> $O/emulate.err || exit $?; grep '^{' $O/run.log | sed "s/^{/{\"streamk_max_cus\": \"${TENSILE_STREAMK_MAX_CUS:-all}\", /" >> $O/emulate.jsonl || exit $?; }
 for c in all 240 224; do
   for lc in 1 16; do
     if [ $c = all ]; then unset TENSILE_STREAMK_MAX_CUS; else export TENSILE_STREAMK_MAX_CUS=$c; fi
