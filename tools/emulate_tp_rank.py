@@ -73,13 +73,19 @@ class _Link:
         self.bps = gbps * 1e9
         self.cus = max(1, int(cus))
         self.stream = torch.cuda.Stream(priority=-1)
+        self.copy_stream = torch.cuda.Stream(priority=-1)
         self.src = torch.zeros(self.cus * 4096, dtype=torch.uint8, device="cuda")
         self.dst = torch.empty_like(self.src)
         self.busy_s = 0.0
 
     def run(self, nbytes: float, work):
+        """Spin for the link time on the link stream and do the receiving-side write on a second
+        side stream, both after the producer: RCCL writes the output while it transfers, so the
+        write must not queue behind the spin (round-4 first traces serialised them: the copies
+        added ~40 % to the link stream's busy time, profiles/r4_stream_timeline_8layers.jsonl)."""
         cur = torch.cuda.current_stream()
         self.stream.wait_stream(cur)
+        self.copy_stream.wait_stream(cur)
         t = nbytes / self.bps
         self.busy_s += t
         with torch.cuda.stream(self.stream):
@@ -87,10 +93,14 @@ class _Link:
                 torch.cuda._sleep(max(1, int(t * self.cycles_per_s)))
             else:
                 self.C.cu_stream(self.src, self.dst, 4096, self.cus, max(1, int(t * 1e8)))
+        with torch.cuda.stream(self.copy_stream):
             work()
         ev = torch.cuda.Event()
         ev.record(self.stream)
-        return ev
+        self.stream.wait_stream(self.copy_stream)   # the handle's event covers the write too
+        ev2 = torch.cuda.Event()
+        ev2.record(self.stream)
+        return ev2
 
 
 _LINK = None
@@ -122,6 +132,7 @@ def _collective(nbytes, work, async_op, tensors):
     if _SYNC == "record":
         for t in tensors:
             t.record_stream(_LINK.stream)
+            t.record_stream(_LINK.copy_stream)
     h = _Pending(_LINK.run(nbytes, work), tensors)
     if async_op:
         return h

@@ -65,8 +65,16 @@ def main(path, as_json=False):
     end = groups[-1][-1] + 1
     sel = rows[start:end]
     t0, t1 = sel[0][0], max(r[1] for r in sel)
-    # link work = everything on the link model's stream (the spin and the receiving-side copies)
-    lq = {q for s, e, n, q in sel if "cu_stream_kernel" in n}
+    # link work = everything on the link model's streams: the spin's stream and a stream that runs
+    # nothing but copies (the receiving-side writes, on their own side stream since round 4)
+    copyish = ("cu_stream_kernel", "copyBuffer", "elementwise_kernel", "CatArray")
+    per = {}
+    for s_, e_, n, q in sel:
+        c = per.setdefault(q, [0, 0])
+        c[0] += 1
+        c[1] += any(k in n for k in copyish)
+    lq = {q for s_, e_, n, q in sel if "cu_stream_kernel" in n}
+    lq |= {q for q, (tot, cp) in per.items() if lq and cp >= 0.95 * tot}
     link = union([[s, e] for s, e, n, q in sel if q in lq])
     comp = union([[s, e] for s, e, n, q in sel if q not in lq])
     fab = [s for s, e, n, q in sel if "fab::" in n]
