@@ -41,6 +41,11 @@ from typing import Generator, List, Sequence
 import torch
 
 _MODE = os.environ.get("NXD_SP_STREAMS", "1")
+# phase offset between the parts: part i starts after part 0 has taken i * STAGGER steps (one step =
+# one collective-bearing op of a decoder layer: qkv all-gather, o_proj reduce-scatter, gate_up
+# all-gather, down reduce-scatter).  0 = strict alternation; 2 puts one part's MLP beside the other
+# part's attention, so the link always has the other part's collective to carry.
+_STAGGER = int(os.environ.get("NXD_SP_STAGGER", "0") or 0)
 _active = False           # inside an interleaved forward/backward (set until join())
 _streams = {}             # device index -> [stream A, stream B]
 
@@ -78,9 +83,15 @@ def streams_for(device: torch.device, n: int = 2) -> List[torch.cuda.Stream]:
     return s[:n]
 
 
+def set_stagger(n: int) -> None:
+    global _STAGGER
+    _STAGGER = max(0, int(n))
+
+
 def run_interleaved(gens: Sequence[Generator], device: torch.device) -> list:
     """Drive the generators alternately (one step each in turn) until all return; generator i
-    runs on stream i (GPU) or inline (CPU).  Returns their return values."""
+    runs on stream i (GPU) or inline (CPU), and joins the rotation once generator 0 has taken
+    i * stagger steps (NXD_SP_STAGGER).  Returns their return values."""
     global _active
     results = [None] * len(gens)
     live = list(range(len(gens)))
@@ -91,8 +102,13 @@ def run_interleaved(gens: Sequence[Generator], device: torch.device) -> list:
         for s in ss:
             s.wait_stream(main)   # weights / zeroed grads / inputs written on the caller's stream
         _active = True
+    steps0 = 0
     while live:
         for i in list(live):
+            if i > 0 and 0 in live and steps0 <= i * _STAGGER:
+                continue   # part i has not joined the rotation yet
+            if i == 0:
+                steps0 += 1
             try:
                 if cuda:
                     with torch.cuda.stream(ss[i]):

@@ -10,7 +10,7 @@ import torch
 from dist_utils import run_distributed
 
 
-def _w(rank, world, streams, out, preset="tiny8"):
+def _w(rank, world, streams, out, preset="tiny8", stagger=0):
     from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import LlamaForCausalLM, llama_config
     from neuronx_distributed_llama3_2_amd.optimizer.flat_optimizer import FlatMixedPrecisionAdamW
     from neuronx_distributed_llama3_2_amd.parallel.grad_buffer import find_shared_params
@@ -18,6 +18,7 @@ def _w(rank, world, streams, out, preset="tiny8"):
     from neuronx_distributed_llama3_2_amd.parallel_layers import stream_split
 
     stream_split.set_enabled(streams >= 2, streams)
+    stream_split.set_stagger(stagger)
     ps.initialize_model_parallel(world)
     cfg = llama_config(preset, sequence_parallel_enabled=True, max_position_embeddings=128, num_hidden_layers=2)
     torch.manual_seed(0)
@@ -48,9 +49,9 @@ def _w(rank, world, streams, out, preset="tiny8"):
         torch.save({"loss": losses, "gn": norms, "interleaved": len(calls)}, out)
 
 
-def _run(world, streams, preset="tiny8"):
+def _run(world, streams, preset="tiny8", stagger=0):
     d = tempfile.mkdtemp()
-    run_distributed(_w, world, streams, os.path.join(d, "r.pt"), preset)
+    run_distributed(_w, world, streams, os.path.join(d, "r.pt"), preset, stagger)
     return torch.load(os.path.join(d, "r.pt"))
 
 
@@ -74,6 +75,15 @@ def test_interleaved_halves_match_one_pass_tp4_replicated_kv():
 def test_four_parts_match_one_pass_tp2():
     # NXD_SP_STREAMS=4: the micro-batch of 4 as four parts on four streams
     a, b = _run(2, 1), _run(2, 4)
+    assert b["interleaved"] == 3
+    for i in range(3):
+        assert abs(a["loss"][i] - b["loss"][i]) < 1e-4 * abs(a["loss"][i]), (a, b)
+        assert abs(a["gn"][i] - b["gn"][i]) < 1e-3 * a["gn"][i], (a, b)
+
+
+def test_staggered_halves_match_one_pass_tp2():
+    # NXD_SP_STAGGER=2: the second half starts two collective steps (half a layer) behind
+    a, b = _run(2, 1), _run(2, 2, stagger=2)
     assert b["interleaved"] == 3
     for i in range(3):
         assert abs(a["loss"][i] - b["loss"][i]) < 1e-4 * abs(a["loss"][i]), (a, b)

@@ -199,6 +199,7 @@ def main():
                     help="collective buffer lifetime: stash until wait() (RCCL default) or record_stream")
     ap.add_argument("--spin", choices=["realtime", "sleep"], default="realtime",
                     help="link spin: real-time-counter copy kernel, or round-3's torch.cuda._sleep")
+    ap.add_argument("--sp-stagger", type=int, default=None, help="NXD_SP_STAGGER for this run")
     ap.add_argument("--sp-streams", type=int, default=None, help="NXD_SP_STREAMS for this run (1 = one pass, k >= 2 parts)")
     a = ap.parse_args()
 
@@ -223,6 +224,10 @@ def main():
         from neuronx_distributed_llama3_2_amd.parallel_layers import stream_split
 
         stream_split.set_enabled(a.sp_streams >= 2, a.sp_streams)
+    if a.sp_stagger is not None:
+        from neuronx_distributed_llama3_2_amd.parallel_layers import stream_split
+
+        stream_split.set_stagger(a.sp_stagger)
     if a.link_gbps and use_cuda:
         _LINK = _Link(a.link_gbps, a.link_cus, a.spin)
     ps.initialize_model_parallel(tensor_model_parallel_size=a.tp)
@@ -288,6 +293,8 @@ def main():
            "link_cus": a.link_cus if _LINK else None, "gemm_no_streamk": os.environ.get("NXD_GEMM_NO_STREAMK", "0"), "spin": a.spin if _LINK else None, "sync": a.sync,
            "sp_streams": __import__("neuronx_distributed_llama3_2_amd.parallel_layers.stream_split",
                                      fromlist=["x"]).parts(),
+           "sp_stagger": __import__("neuronx_distributed_llama3_2_amd.parallel_layers.stream_split",
+                                    fromlist=["x"])._STAGGER,
            "link_busy_ms_per_step": round(1000 * _LINK.busy_s / (a.warmup + a.steps), 2) if _LINK else None,
            "ms_per_step": round(1000 * el, 2), "ms_per_microbatch": round(1000 * el / accum, 2),
            "node_tokens_per_s_comm_free": round(a.gbs * a.seq / el, 1),
