@@ -974,13 +974,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("nq"), py::arg("nkv"), py::arg("D"), py::arg("cos_t"), py::arg("sin_t"), py::arg("pos"), py::arg("T"),
         py::arg("kc"), py::arg("vc"), py::arg("cache_idx"), py::arg("xadd") = py::none(), py::arg("yadd") = py::none());
   // decode A/B knobs: 0 = GLU row pairs per wave, 1 = GEMV k-slices (0 auto), 2 = MFMA decode attention on/off,
-  // 3 = GEMV early epilogue / prologue reads on/off, 4 = non-temporal weight loads on/off,
-  // 5 = persistent GEMV grid (workgroups per CU; 0 = off)
+  // 3 = GEMV early epilogue / prologue reads on/off, 4 = non-temporal weight loads on/off
   m.def("decode_set_knob", [](int which, int value) {
     if (which == 2) nxd::decode_attn_set_v2(value);
     else if (which == 3) nxd::dgemv_set_knob(2, value);
     else if (which == 4) nxd::dgemv_set_knob(3, value);
-    else if (which == 5) nxd::dgemv_set_knob(4, value);
     else nxd::dgemv_set_knob(which, value);
   });
   m.doc() = "CDNA4 (gfx950) kernels of neuronx_distributed_llama3_2_amd";

@@ -331,283 +331,6 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
   }
 }
 
-// Persistent variant (NXD_DECODE_PERSIST=1, A/B): a grid of a few workgroups per CU loops over the
-// row groups, issuing the NEXT group's weight rows (register double buffer) before the current
-// group's FMAs, reduction and epilogue, and builds the normalised activation image in LDS once per
-// workgroup instead of once per row group -- the weight stream does not drain between wave
-// generations.  Single load round per row group (K / KS <= U * 512); the epilogue's own operands
-// (residual row, pending o_proj sum, cos / sin) are read right after the next group's weights.
-template <int MM, int NW, int EPI, bool NORM, int KS>
-__global__ void __launch_bounds__(256) dgemv_persist_kernel(Params p, int groups) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* xs = reinterpret_cast<uint16_t*>(smem);
-  __shared__ float red[4][MM];
-  __shared__ float part[4][MM][NW];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int rg = wid / KS, ks = wid % KS;
-  constexpr int RPW = 4 / KS;   // row groups per workgroup iteration
-  const int kc = ((p.K + KS - 1) / KS + 7) & ~7;
-  const int kbeg = min(ks * kc, p.K), kend = min(p.K, kbeg + kc);
-
-  auto setup = [&](int wave, int* rows, bool& active) {
-    if (EPI == GLU) {
-      active = wave * (NW / 2) < p.N;
-#pragma unroll
-      for (int i = 0; i < NW / 2; ++i) {
-        rows[2 * i] = min(wave * (NW / 2) + i, p.N - 1);
-        rows[2 * i + 1] = rows[2 * i] + p.N;
-      }
-    } else if (EPI == ROPE_KV) {
-      const int half = p.D / 2;
-      const int npair = (p.nq + p.nkv) * half;
-      const int nv = p.nkv * p.D;
-      active = true;
-      if (wave < npair) {
-        const int h = wave / half, d = wave % half;
-        rows[0] = h * p.D + d;
-        rows[1] = rows[0] + half;
-      } else {
-        const int r = (p.nq + p.nkv) * p.D + 2 * (wave - npair);
-        active = (wave - npair) * 2 < nv;
-        rows[0] = min(r, p.N - 1);
-        rows[1] = min(r + 1, p.N - 1);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NW; ++i) rows[i] = min(wave * NW + i, p.N - 1);
-      active = wave * NW < p.N;
-    }
-  };
-  auto load = [&](u32x4_t (&dst)[NW][U], const int* rows) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = kbeg + lane * 8 + u * 512;
-#pragma unroll
-      for (int r = 0; r < NW; ++r)
-        dst[r][u] = k < kend ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p.w + (int64_t)rows[r] * p.ldw + k))
-                             : u32x4_t{0, 0, 0, 0};
-    }
-  };
-
-  int it = blockIdx.x;
-  if (it * RPW >= groups) return;
-  int rows[NW];
-  bool active;
-  setup(it * RPW + rg, rows, active);
-  u32x4_t wv[NW][U], wn[NW][U];
-  load(wv, rows);
-
-  if (NORM) {   // normalised activation rows in LDS, once per workgroup
-    float ss[MM];
-#pragma unroll
-    for (int m = 0; m < MM; ++m) ss[m] = 0.f;
-    for (int k = tid * 8; k < p.K; k += 256 * 8) {
-#pragma unroll
-      for (int m = 0; m < MM; ++m) {
-        if (m < p.M) {
-          u32x4_t v = *reinterpret_cast<const u32x4_t*>(p.x + (int64_t)m * p.ldx + k);
-          float f[8];
-          unpack8(v, f);
-          if (p.xadd) {
-            const f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k);
-            const f32x4_t a1 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k + 4);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = bf2f(f2bf(f[j] + bf2f(f2bf(j < 4 ? a0[j] : a1[j - 4]))));
-            v = pack8(f);
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ss[m] += f[j] * f[j];
-          *reinterpret_cast<u32x4_t*>(xs + m * p.K + k) = v;
-        }
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < MM; ++m) {
-      const float sm = wave_sum(ss[m]);
-      if (lane == 0) red[wid][m] = sm;
-    }
-    __syncthreads();
-    float rstd[MM];
-#pragma unroll
-    for (int m = 0; m < MM; ++m) rstd[m] = rsqrtf((red[0][m] + red[1][m] + red[2][m] + red[3][m]) / (float)p.K + p.eps);
-    for (int k = tid * 8; k < p.K; k += 256 * 8) {
-      float g[8];
-      unpack8(*reinterpret_cast<const u32x4_t*>(p.norm_w + k), g);
-#pragma unroll
-      for (int m = 0; m < MM; ++m) {
-        if (m < p.M) {
-          float f[8];
-          unpack8(*reinterpret_cast<const u32x4_t*>(xs + m * p.K + k), f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = f[j] * rstd[m] * g[j];
-          *reinterpret_cast<u32x4_t*>(xs + m * p.K + k) = pack8(f);
-        }
-      }
-    }
-    __syncthreads();
-  }
-
-  for (;;) {
-    const int wave = it * RPW + rg;
-    const int nit = it + gridDim.x;
-    const bool more = nit * RPW < groups;   // workgroup-uniform
-    int nrows[NW];
-    bool nactive = false;
-    if (more) {
-      setup(nit * RPW + rg, nrows, nactive);
-      load(wn, nrows);
-    }
-    // this group's epilogue operands, in flight beside the next group's weights
-    float y_pre[MM][NW], ya_pre[MM][NW], cs_pre[MM], sn_pre[MM];
-    if (lane == 0 && active && (KS == 1 || ks == 0)) {
-#pragma unroll
-      for (int m = 0; m < MM; ++m) {
-        if (m >= p.M) continue;
-        if (EPI == RESID) {
-#pragma unroll
-          for (int r = 0; r < NW; ++r) {
-            const int n = min(wave * NW + r, p.N - 1);
-            y_pre[m][r] = bf2f(p.y[(int64_t)m * p.ldy + n]);
-            ya_pre[m][r] = p.yadd ? p.yadd[(int64_t)m * p.N + n] : 0.f;
-          }
-        } else if (EPI == ROPE_KV) {
-          const int half = p.D / 2;
-          if (rows[0] < (p.nq + p.nkv) * p.D && rows[1] == rows[0] + half) {
-            const int64_t ps = p.pos[m];
-            const int64_t pt = ps < 0 ? 0 : (ps >= p.max_pos ? p.max_pos - 1 : ps);
-            const int d = rows[0] % p.D;
-            cs_pre[m] = p.cos_t[pt * half + d];
-            sn_pre[m] = p.sin_t[pt * half + d];
-          }
-        }
-      }
-    }
-    float acc[MM][NW];
-#pragma unroll
-    for (int m = 0; m < MM; ++m)
-#pragma unroll
-      for (int r = 0; r < NW; ++r) acc[m][r] = 0.f;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = kbeg + lane * 8 + u * 512;
-      if (k < kend) {
-#pragma unroll
-        for (int m = 0; m < MM; ++m) {
-          if (m < p.M) {
-            float xf[8];
-            const uint16_t* xp = NORM ? (xs + m * p.K + k) : (p.x + (int64_t)m * p.ldx + k);
-            unpack8(*reinterpret_cast<const u32x4_t*>(xp), xf);
-#pragma unroll
-            for (int r = 0; r < NW; ++r) {
-              float wf[8];
-              unpack8(wv[r][u], wf);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) acc[m][r] += xf[e] * wf[e];
-            }
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < MM; ++m)
-#pragma unroll
-      for (int r = 0; r < NW; ++r) acc[m][r] = wave_sum(acc[m][r]);
-    bool writer = lane == 0 && active;
-    if (KS > 1) {
-      if (lane == 0) {
-#pragma unroll
-        for (int m = 0; m < MM; ++m)
-#pragma unroll
-          for (int r = 0; r < NW; ++r) part[wid][m][r] = acc[m][r];
-      }
-      __syncthreads();
-      if (ks == 0) {
-#pragma unroll
-        for (int m = 0; m < MM; ++m)
-#pragma unroll
-          for (int r = 0; r < NW; ++r) {
-            float t = 0.f;
-#pragma unroll
-            for (int j = 0; j < KS; ++j) t += part[wid + j][m][r];
-            acc[m][r] = t;
-          }
-      }
-      writer = writer && ks == 0;
-    }
-    if (writer) {
-#pragma unroll
-      for (int m = 0; m < MM; ++m) {
-        if (m >= p.M) continue;
-        uint16_t* yr = p.y + (int64_t)m * p.ldy;
-        if (EPI == GLU) {
-#pragma unroll
-          for (int i = 0; i < NW / 2; ++i) {
-            if (wave * (NW / 2) + i >= p.N) continue;
-            const float g = acc[m][2 * i], u = acc[m][2 * i + 1];
-            yr[rows[2 * i]] = f2bf(g / (1.f + __expf(-g)) * u);
-          }
-        } else if (EPI == ROPE_KV) {
-          const int half = p.D / 2;
-          const int64_t ps = p.pos[m];
-          const int b = m / p.T;
-          const int cb = p.cache_idx ? p.cache_idx[b] : b;
-          const bool in_cache = ps >= 0 && ps < p.Lmax;
-          const int qk_rows = (p.nq + p.nkv) * p.D;
-          if (rows[0] < qk_rows && rows[1] == rows[0] + half) {
-            const int h = rows[0] / p.D, d = rows[0] % p.D;
-            const float x1 = bf2f(f2bf(acc[m][0])), x2 = bf2f(f2bf(acc[m][1]));
-            const uint16_t o1 = f2bf(x1 * cs_pre[m] - x2 * sn_pre[m]), o2 = f2bf(x2 * cs_pre[m] + x1 * sn_pre[m]);
-            yr[rows[0]] = o1;
-            yr[rows[1]] = o2;
-            if (h >= p.nq && in_cache) {
-              uint16_t* kp = p.kc + (int64_t)cb * p.c_sb + (int64_t)(h - p.nq) * p.c_sh + ps * p.c_sl;
-              kp[d] = o1;
-              kp[d + half] = o2;
-            }
-          } else {
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-              if (r == 1 && rows[1] == rows[0]) break;
-              const uint16_t o = f2bf(acc[m][r]);
-              yr[rows[r]] = o;
-              const int vr = rows[r] - qk_rows;
-              if (in_cache)
-                p.vc[(int64_t)cb * p.c_sb + (int64_t)(vr / p.D) * p.c_sh + ps * p.c_sl + vr % p.D] = o;
-            }
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < NW; ++r) {
-            const int n = wave * NW + r;
-            if (n >= p.N) continue;
-            if (EPI == RESID) {
-              float yv = y_pre[m][r];
-              if (p.yadd) {
-                yv = bf2f(f2bf(yv + bf2f(f2bf(ya_pre[m][r]))));
-                p.yadd[(int64_t)m * p.N + n] = 0.f;
-              }
-              yr[n] = f2bf(yv + bf2f(f2bf(acc[m][r])));
-            } else {
-              yr[n] = f2bf(acc[m][r]);
-            }
-          }
-        }
-      }
-    }
-    if (!more) break;
-    if (KS > 1) __syncthreads();   // part[] is rewritten next iteration
-    it = nit;
-    active = nactive;
-#pragma unroll
-    for (int r = 0; r < NW; ++r) {
-      rows[r] = nrows[r];
-#pragma unroll
-      for (int u = 0; u < U; ++u) wv[r][u] = wn[r][u];
-    }
-  }
-}
-
-int g_persist = -1;    // NXD_DECODE_PERSIST: persistent GEMV grid (workgroups per CU, 0 = off)
 
 // k-slices per row group: split K while the grid stays <= 8192 waves and slices keep >= 1024
 // elements (o_proj 2048 x 2048 -> 2, down 2048 x 8192 -> 4, gate_up / lm_head -> 1)
@@ -640,27 +363,6 @@ static int launch(const Params& p, int groups, hipStream_t s) {
   const size_t lds = NORM ? (size_t)MM * p.K * 2 : 0;
   const int ks = pick_ks(groups, p.K, EPI);
   const dim3 grid((unsigned)((groups * ks + 3) / 4)), block(256);
-  if (g_persist < 0) {
-    const char* e = getenv("NXD_DECODE_PERSIST");
-    g_persist = e ? atoi(e) : 0;
-  }
-  if constexpr (MM <= 2) if (g_persist > 0 && p.K <= ks * U * 512) {
-    static int ncu = 0;
-    if (ncu == 0) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-    }
-    const int rpw = 4 / ks;
-    const int wgs = min((groups + rpw - 1) / rpw, ncu * g_persist);
-    if (ks == 4)
-      hipLaunchKernelGGL((dgemv_persist_kernel<MM, NW, EPI, NORM, 4>), dim3(wgs), block, lds, s, p, groups);
-    else if (ks == 2)
-      hipLaunchKernelGGL((dgemv_persist_kernel<MM, NW, EPI, NORM, 2>), dim3(wgs), block, lds, s, p, groups);
-    else
-      hipLaunchKernelGGL((dgemv_persist_kernel<MM, NW, EPI, NORM, 1>), dim3(wgs), block, lds, s, p, groups);
-    return hipGetLastError() == hipSuccess ? 0 : 1;
-  }
   if (ks == 4)
     hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 4>), grid, block, lds, s, p);
   else if (ks == 2)
@@ -702,7 +404,6 @@ void dgemv_set_knob(int which, int value) {
   else if (which == 1) dfused::g_ks = value;
   else if (which == 2) dfused::g_pf = value != 0;
   else if (which == 3) dfused::g_nt = value != 0;
-  else if (which == 4) dfused::g_persist = value;
 }
 
 int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,

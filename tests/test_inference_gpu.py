@@ -370,38 +370,3 @@ def test_greedy_fused_decode_matches_unfused(hf_sd):
         finally:
             graphs.GREEDY_FUSED = True
     assert torch.equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("wgs", [1, 2, 4])
-def test_persistent_decode_gemv_is_bit_exact(wgs):
-    """NXD_DECODE_PERSIST (decode_fused.hip dgemv_persist_kernel: a few workgroups per CU loop over
-    the row groups with the next group's weights in flight) does the same arithmetic in the same
-    order as the one-group-per-wave kernel: greedy tokens and decode logits are bit-identical."""
-    from transformers import LlamaConfig, LlamaForCausalLM as HF
-
-    from neuronx_distributed_llama3_2_amd.ops._ext import ext
-
-    cfg = LlamaConfig(hidden_size=1024, intermediate_size=2048, num_hidden_layers=2, num_attention_heads=16,
-                      num_key_value_heads=4, vocab_size=1000, max_position_embeddings=1024, rms_norm_eps=1e-5,
-                      rope_theta=500000.0, tie_word_embeddings=True, eos_token_id=2)
-    torch.manual_seed(0)
-    sd = {k: v.detach().clone() for k, v in HF(cfg).state_dict().items()}
-    torch.manual_seed(5)
-    ids = torch.randint(3, cfg.vocab_size, (1, 33))
-    outs, logits = [], []
-    try:
-        for n in (0, wgs):
-            ext().decode_set_knob(5, n)
-            m = _model(cfg, sd, torch.bfloat16, graphs=True, steps=4, device=torch.device("cuda"))
-            m.config.deterministic = True
-            m.model._decode_deterministic = True   # no fp32-atomic attention + o_proj launch
-            outs.append(m.generate(ids, max_new_tokens=16, eos_token_id=-1).cpu())
-            assert m.model._decode_fused_ok is True
-            last = outs[-1][:, -1:].cuda()
-            pos = torch.full((1, 1), outs[-1].shape[1] - 1, dtype=torch.int64, device="cuda")
-            clen = torch.full((1,), outs[-1].shape[1], dtype=torch.int32, device="cuda")
-            logits.append(m.model.forward_tokens(last, pos, torch.arange(1, device="cuda"), clen).float().cpu())
-    finally:
-        ext().decode_set_knob(5, 0)
-    assert torch.equal(outs[0], outs[1])
-    assert torch.equal(logits[0], logits[1])
