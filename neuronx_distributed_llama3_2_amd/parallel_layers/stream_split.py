@@ -43,9 +43,11 @@ import torch
 _MODE = os.environ.get("NXD_SP_STREAMS", "1")
 # phase offset between the parts: part i starts after part 0 has taken i * STAGGER steps (one step =
 # one collective-bearing op of a decoder layer: qkv all-gather, o_proj reduce-scatter, gate_up
-# all-gather, down reduce-scatter).  0 = strict alternation; 2 puts one part's MLP beside the other
-# part's attention, so the link always has the other part's collective to carry.
-_STAGGER = int(os.environ.get("NXD_SP_STAGGER", "0") or 0)
+# all-gather, down reduce-scatter).  0 = strict alternation; 2 (default) puts one part's MLP beside
+# the other part's attention.  Emulated ranks, stagger 2 vs 0 (profiles/r4_emulate_sp_stagger.jsonl):
+# TP=8 at 400 GB/s 516 vs 518 ms, without links 386 vs 397; TP=4 at 200 GB/s 898 vs 931; TP=2 at
+# 70 GB/s 1,753 vs 1,801.
+_STAGGER = int(os.environ.get("NXD_SP_STAGGER", "2") or 0)
 _active = False           # inside an interleaved forward/backward (set until join())
 _streams = {}             # device index -> [stream A, stream B]
 
