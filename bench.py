@@ -335,7 +335,7 @@ def main(a):
             "num_alloc_retries": int(ms1.get("num_alloc_retries", 0) - ms0.get("num_alloc_retries", 0)),
             "rccl_max_channels": os.environ.get("NCCL_MAX_NCHANNELS", "rccl default"),
             "streamk_max_cus": os.environ.get("TENSILE_STREAMK_MAX_CUS", "all"),
-            "sp_streams": stream_split.parts() if over["sequence_parallel_enabled"] else 1,
+            "sp_streams": stream_split.parts() if (over["sequence_parallel_enabled"] or stream_split.without_sp()) else 1,
             "api": "nxd.initialize_parallel_model / initialize_parallel_optimizer",
         }
         print(json.dumps(rec), flush=True)

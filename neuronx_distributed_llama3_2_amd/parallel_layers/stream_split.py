@@ -52,6 +52,15 @@ _active = False           # inside an interleaved forward/backward (set until jo
 _streams = {}             # device index -> [stream A, stream B]
 
 
+_NO_SP = os.environ.get("NXD_SP_STREAMS_NO_SP", "0") == "1"
+
+
+def without_sp() -> bool:
+    """NXD_SP_STREAMS_NO_SP=1: also split micro-batches that run without sequence parallelism
+    (TP = 1): the parts' kernels then only share the GPU, no collectives to hide (experiment)."""
+    return _NO_SP
+
+
 def parts() -> int:
     """Streams (micro-batch parts) requested: 1 = off."""
     try:
