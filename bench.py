@@ -37,6 +37,10 @@ os.environ.setdefault("NXD_LOG_STREAM", "stderr")
 # 601 -> 532 ms per step, TP=2 over its one xGMI link 4488 -> 1839; bit-identical across runs on the
 # GPU kernels).  Library default is one pass; NXD_SP_STREAMS=1 restores it here.
 os.environ.setdefault("NXD_SP_STREAMS", "2")
+# TP = 1 (one GPU) runs the same two staggered halves without collectives: their kernels only share
+# the GPU (a GEMM of one half beside the other's attention / norm / SwiGLU): 3,071 -> 3,018 ms per
+# step, same loss, alternating A/B on one box (profiles/r4_tp1_halves_bench_ab.txt).
+os.environ.setdefault("NXD_SP_STREAMS_NO_SP", "1")
 
 # Micro-batch per TP degree: TP shrinks every per-rank GEMM and the attention head count, so the
 # TP>1 ranks process several sequences per micro-batch to keep MFMA tiles and the attention grid
