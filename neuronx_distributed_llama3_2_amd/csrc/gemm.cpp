@@ -103,6 +103,7 @@ class Tuner {
   }
 
   size_t max_ws() const { return ws_limit_; }
+  int retime() const { return retime_; }
   int candidates() const { return candidates_; }
   int mode() const { return mode_; }
 
@@ -150,6 +151,8 @@ class Tuner {
     candidates_ = c ? std::max(1, std::atoi(c)) : 24;
     const char* f = std::getenv("NXD_GEMM_TUNE_FILE");
     if (f) file_ = f;
+    const char* rt = std::getenv("NXD_GEMM_RETIME");
+    retime_ = rt ? std::max(0, std::atoi(rt)) : 3;
     const char* w = std::getenv("NXD_GEMM_WORKSPACE_MB");
     ws_limit_ = (size_t)(w ? std::atoi(w) : 128) << 20;
   }
@@ -201,7 +204,7 @@ class Tuner {
   std::unordered_set<std::string> logged_;
   int max_algos_ = 4096;
   bool loaded_ = false;
-  int mode_ = 1, candidates_ = 24;
+  int mode_ = 1, candidates_ = 24, retime_ = 3;
   size_t ws_limit_ = 128u << 20;
 };
 
@@ -521,16 +524,39 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
       const double flops = 2.0 * M * N * K;
       const int reps = flops > 1e12 ? 3 : (flops > 1e10 ? 8 : 20);
       best = -1;
+      std::vector<std::pair<float, int>> first;
       for (int i = 0; i < got; ++i) {
         if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > wsmax || skip[i]) continue;
         float ms = time_algo(h, ds, res[i].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(), c.data_ptr(), Dp, ws,
                              wsmax, s, reps);
+        if (ms > 0.f) first.emplace_back(ms, i);
         if (ms > 0.f && (best < 0 || ms < best_ms)) {
           best = i;
           best_ms = ms;
         }
       }
       TORCH_CHECK(best >= 0, "gemm: every candidate failed for ", key);
+      // re-time the leaders round-robin (NXD_GEMM_RETIME rounds, default 3): one short timing per
+      // candidate drifts with the clock the chip holds at that moment, so near-ties are decided by
+      // the minimum over interleaved rounds instead of by whichever ran first
+      if (T.retime() > 0 && first.size() > 1) {
+        std::sort(first.begin(), first.end());
+        const size_t nl = std::min<size_t>(3, first.size());
+        std::vector<float> bestr(nl, 1e30f);
+        for (int r = 0; r < T.retime(); ++r)
+          for (size_t j = 0; j < nl; ++j) {
+            const float ms = time_algo(h, ds, res[first[j].second].algo, &alpha, &beta, b.data_ptr(), a.data_ptr(),
+                                       c.data_ptr(), Dp, ws, wsmax, s, reps);
+            if (ms > 0.f) bestr[j] = std::min(bestr[j], ms);
+          }
+        size_t w = 0;
+        for (size_t j = 1; j < nl; ++j)
+          if (bestr[j] < bestr[w]) w = j;
+        if (bestr[w] < 1e29f) {
+          best = first[w].second;
+          best_ms = bestr[w];
+        }
+      }
     }
     ch.algo = res[best].algo;
     ch.ws = res[best].workspaceSize;
