@@ -152,7 +152,7 @@ class Tuner {
     const char* f = std::getenv("NXD_GEMM_TUNE_FILE");
     if (f) file_ = f;
     const char* rt = std::getenv("NXD_GEMM_RETIME");
-    retime_ = rt ? std::max(0, std::atoi(rt)) : 3;
+    retime_ = rt ? std::max(0, std::atoi(rt)) : 0;
     const char* w = std::getenv("NXD_GEMM_WORKSPACE_MB");
     ws_limit_ = (size_t)(w ? std::atoi(w) : 128) << 20;
   }
@@ -204,7 +204,7 @@ class Tuner {
   std::unordered_set<std::string> logged_;
   int max_algos_ = 4096;
   bool loaded_ = false;
-  int mode_ = 1, candidates_ = 24, retime_ = 3;
+  int mode_ = 1, candidates_ = 24, retime_ = 0;
   size_t ws_limit_ = 128u << 20;
 };
 
@@ -536,9 +536,10 @@ void gemm(at::Tensor a, at::Tensor b, at::Tensor d, c10::optional<at::Tensor> c_
         }
       }
       TORCH_CHECK(best >= 0, "gemm: every candidate failed for ", key);
-      // re-time the leaders round-robin (NXD_GEMM_RETIME rounds, default 3): one short timing per
+      // optional (NXD_GEMM_RETIME=n rounds): re-time the leaders round-robin -- one short timing per
       // candidate drifts with the clock the chip holds at that moment, so near-ties are decided by
-      // the minimum over interleaved rounds instead of by whichever ran first
+      // the minimum over interleaved rounds.  1-GPU bench with 3 rounds vs none: 3,031 / 3,032 vs
+      // 3,027 / 3,031 ms per step (profiles/r4_gemm_retime_bench_ab.txt), so off by default.
       if (T.retime() > 0 && first.size() > 1) {
         std::sort(first.begin(), first.end());
         const size_t nl = std::min<size_t>(3, first.size());
