@@ -955,6 +955,26 @@ PYBIND11_MODULE(_C, m) {
   m.def("grouped_gemm", &grouped_gemm);
   m.def("wgrad_gemm", &wgrad_gemm);
   // diagnostics: copy kernel on exactly `blocks` workgroups (CU-interference measurements)
+  // A HIP stream whose kernels may only use the CUs whose bits are NOT listed in `exclude`
+  // (hipExtStreamCreateWithCUMask; the CUs left out stay free for the collectives' kernels, which
+  // then never wait for a compute workgroup to retire).  Returns the raw stream handle for
+  // torch.cuda.ExternalStream; the stream lives for the process.
+  m.def("cu_masked_stream", [](std::vector<int64_t> exclude) {
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    TORCH_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0,
+                "cu_masked_stream: CU count");
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
+    for (int64_t c : exclude) {
+      TORCH_CHECK(c >= 0 && c < ncu, "cu_masked_stream: CU index out of range");
+      mask[c / 32] &= ~(1u << (c % 32));
+    }
+    hipStream_t st = nullptr;
+    check_rc(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) == hipSuccess ? 0 : -1,
+             "hipExtStreamCreateWithCUMask");
+    return (int64_t)(uintptr_t)st;
+  });
   m.def("cu_stream", [](at::Tensor src, at::Tensor dst, int64_t bytes_per_block, int64_t blocks, int64_t ticks) {
     check_cuda(src, "src");
     check_cuda(dst, "dst");

@@ -53,6 +53,22 @@ _streams = {}             # device index -> [stream A, stream B]
 
 
 _NO_SP = os.environ.get("NXD_SP_STREAMS_NO_SP", "0") == "1"
+# NXD_SP_RESERVE_CUS=n: the parts' streams are CU-masked to leave n CUs (spread over the XCDs) to the
+# collectives, whose kernels otherwise wait for a compute workgroup to retire before they can start
+# (every heavy kernel holds whole CUs: 256-thread workgroups at the register / LDS maximum)
+_RESERVE = int(os.environ.get("NXD_SP_RESERVE_CUS", "0") or 0)
+
+
+def reserved_cus(n: int, ncu: int = 256) -> List[int]:
+    """n CU indices spread over the 8 XCDs whether the mask bits are XCD-major (32 per XCD) or
+    XCD-interleaved (bit i on XCD i % 8): index 32 j + j (+ 8 k) lands on XCD j either way."""
+    per = ncu // 8
+    out = []
+    for k in range((n + 7) // 8):
+        for j in range(8):
+            if len(out) < n:
+                out.append(per * j + j + 8 * k)
+    return out
 
 
 def without_sp() -> bool:
@@ -90,7 +106,15 @@ def streams_for(device: torch.device, n: int = 2) -> List[torch.cuda.Stream]:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _streams.setdefault(idx, [])
     while len(s) < n:
-        s.append(torch.cuda.Stream(device=idx))
+        if _RESERVE > 0:
+            from ..ops._ext import ext
+
+            with torch.cuda.device(idx):
+                ncu = torch.cuda.get_device_properties(idx).multi_processor_count
+                h = ext().cu_masked_stream(reserved_cus(_RESERVE, ncu))
+                s.append(torch.cuda.ExternalStream(h, device=torch.device("cuda", idx)))
+        else:
+            s.append(torch.cuda.Stream(device=idx))
     return s[:n]
 
 
