@@ -55,7 +55,9 @@ _streams = {}             # device index -> [stream A, stream B]
 _NO_SP = os.environ.get("NXD_SP_STREAMS_NO_SP", "0") == "1"
 # NXD_SP_RESERVE_CUS=n: the parts' streams are CU-masked to leave n CUs (spread over the XCDs) to the
 # collectives, whose kernels otherwise wait for a compute workgroup to retire before they can start
-# (every heavy kernel holds whole CUs: 256-thread workgroups at the register / LDS maximum)
+# (every heavy kernel holds whole CUs: 256-thread workgroups at the register / LDS maximum).
+# Measured slower, off: emulated TP=8 without links 387 -> 467 ms with 8 CUs masked off (far more
+# than the 3 % of CUs), 518 -> 557 at 400 GB/s (profiles/r4_emulate_cu_masked_streams.jsonl).
 _RESERVE = int(os.environ.get("NXD_SP_RESERVE_CUS", "0") or 0)
 
 
