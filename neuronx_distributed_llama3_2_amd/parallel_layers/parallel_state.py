@@ -119,9 +119,9 @@ def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_mode
     from ..parallel.rccl_env import log_comm_config
 
     log_comm_config()
-    # NXD_GEMM_NO_STREAMK=1: skip stream-K solutions of the heuristic list for runs whose
-    # collectives overlap GEMMs (opt-in; csrc/gemm.cpp)
-    set_overlap_safe(os.environ.get("NXD_GEMM_NO_STREAMK", "0") == "1" and world > 1)
+    # NXD_GEMM_NO_STREAMK=1: skip stream-K solutions of the heuristic list for runs whose GEMMs
+    # overlap other kernels -- collectives, or the other SP part's kernels (opt-in; csrc/gemm.cpp)
+    set_overlap_safe(os.environ.get("NXD_GEMM_NO_STREAMK", "0") == "1")
     _TP_GROUP = _assign(tp_mesh, rank, high_priority=True)
     _DP_GROUP = _assign(dp_mesh, rank)
     _PP_GROUP = _assign(pp_mesh, rank)
