@@ -641,7 +641,8 @@ __global__ void __launch_bounds__(kThreads, 1) bwd_kernel(BwdParams p) {
 template <int D>
 __global__ void __launch_bounds__(256) prep_kernel(const uint16_t* o, const uint16_t* dout, const float* lse, float* nlse,
                                                   float* ndelta, int64_t o_sb, int64_t o_ss, int64_t o_sh, int64_t d_sb,
-                                                  int64_t d_ss, int64_t d_sh, int B, int Sq, int Hq, float inv_scale) {
+                                                  int64_t d_ss, int64_t d_sh, int B, int Sq, int Hq, float inv_scale,
+                                                  float* dq_zero, int Sq_pad) {
   constexpr int LPR = D / 8;
   const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
   const int c = threadIdx.x % LPR;
@@ -651,6 +652,11 @@ __global__ void __launch_bounds__(256) prep_kernel(const uint16_t* o, const uint
     const int b = row / ((int64_t)Hq * Sq);
     const int h = (row / Sq) % Hq;
     const int qi = row % Sq;
+    if (dq_zero != nullptr) {   // this row's slice of the fp32 dQ accumulator (rows >= Sq are never read)
+      float* z = dq_zero + (((int64_t)b * Hq + h) * Sq_pad + qi) * D + c * 8;
+      *reinterpret_cast<f32x4_t*>(z) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4_t*>(z + 4) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
     const u32x4_t ov = *reinterpret_cast<const u32x4_t*>(o + b * o_sb + (int64_t)qi * o_ss + h * o_sh + c * 8);
     const u32x4_t dv = *reinterpret_cast<const u32x4_t*>(dout + b * d_sb + (int64_t)qi * d_ss + h * d_sh + c * 8);
     float of[8], df[8];
@@ -928,8 +934,19 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   const bool slabs = slab_mode() != 0;
   float* dk_slab = slabs ? ndelta + (int64_t)B * Hq * Sq : nullptr;
   float* dv_slab = slabs ? dk_slab + (int64_t)B * Hkv * per_bh * kBlockK * D : nullptr;
-  // one memset for the accumulators (contiguous; the slabs are written whole by the kernel)
-  (void)hipMemsetAsync(ws, 0, (size_t)((int64_t)B * Hq * Sq_pad * D + (slabs ? 0 : 2 * (int64_t)B * Hkv * Sk_pad * D)) * sizeof(float), stream);
+  // zeroing: in slab mode the dQ accumulator's rows are zeroed by the prep kernel (it visits every
+  // (row, head) anyway; a separate memset launch waited behind the other SP half's persistent GEMM
+  // workgroups: 0.33 ms per call in the two-halves step) and the slabs are written whole; the
+  // atomic dK/dV mode memsets everything
+  static int prep_zero = -1;   // NXD_FAB_PREP_ZERO=0: back to one memset (A/B)
+  if (prep_zero < 0) {
+    const char* e = getenv("NXD_FAB_PREP_ZERO");
+    prep_zero = e ? (atoi(e) != 0) : 1;
+  }
+  const bool pz = slabs && prep_zero;
+  if (!pz)
+    (void)hipMemsetAsync(ws, 0, (size_t)((int64_t)B * Hq * Sq_pad * D + (slabs ? 0 : 2 * (int64_t)B * Hkv * Sk_pad * D)) * sizeof(float), stream);
+  float* dq_zero = pz ? dq_acc : nullptr;
 
   const int64_t nrows = (int64_t)B * Hq * Sq;
   const int rows_per_block = 256 / (D / 8);
@@ -937,10 +954,12 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   if (gpre > 0) {
     if (D == 128)
       hipLaunchKernelGGL(prep_kernel<128>, dim3(gpre), dim3(256), 0, stream, (const uint16_t*)o, (const uint16_t*)dout, lse,
-                         nlse, ndelta, os[0], os[1], os[2], dos[0], dos[1], dos[2], B, Sq, Hq, 1.f / softmax_scale);
+                         nlse, ndelta, os[0], os[1], os[2], dos[0], dos[1], dos[2], B, Sq, Hq, 1.f / softmax_scale,
+                         dq_zero, (int)Sq_pad);
     else
       hipLaunchKernelGGL(prep_kernel<64>, dim3(gpre), dim3(256), 0, stream, (const uint16_t*)o, (const uint16_t*)dout, lse,
-                         nlse, ndelta, os[0], os[1], os[2], dos[0], dos[1], dos[2], B, Sq, Hq, 1.f / softmax_scale);
+                         nlse, ndelta, os[0], os[1], os[2], dos[0], dos[1], dos[2], B, Sq, Hq, 1.f / softmax_scale,
+                         dq_zero, (int)Sq_pad);
   }
 
   BwdParams p;
