@@ -934,14 +934,14 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
   const bool slabs = slab_mode() != 0;
   float* dk_slab = slabs ? ndelta + (int64_t)B * Hq * Sq : nullptr;
   float* dv_slab = slabs ? dk_slab + (int64_t)B * Hkv * per_bh * kBlockK * D : nullptr;
-  // zeroing: in slab mode the dQ accumulator's rows are zeroed by the prep kernel (it visits every
-  // (row, head) anyway; a separate memset launch waited behind the other SP half's persistent GEMM
-  // workgroups: 0.33 ms per call in the two-halves step) and the slabs are written whole; the
-  // atomic dK/dV mode memsets everything
-  static int prep_zero = -1;   // NXD_FAB_PREP_ZERO=0: back to one memset (A/B)
+  // zeroing: one memset for the accumulators (the slabs are written whole by the kernel), or, opt-in,
+  // the dQ rows zeroed by the prep kernel, which visits every (row, head) anyway
+  // NXD_FAB_PREP_ZERO=1 zeroes in the prep kernel instead of the memset launch: bench 3,006 / 3,016
+  // vs 2,999 / 3,007 ms per step with the memset (profiles/r4_fab_prep_zero_ab.txt), so off
+  static int prep_zero = -1;
   if (prep_zero < 0) {
     const char* e = getenv("NXD_FAB_PREP_ZERO");
-    prep_zero = e ? (atoi(e) != 0) : 1;
+    prep_zero = e ? (atoi(e) != 0) : 0;
   }
   const bool pz = slabs && prep_zero;
   if (!pz)
