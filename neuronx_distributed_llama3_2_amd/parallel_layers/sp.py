@@ -46,7 +46,10 @@ _SP_CHUNKS = int(os.environ["NXD_SP_CHUNKS"]) if "NXD_SP_CHUNKS" in os.environ e
 # reduce-scatter: a win for any T above ~0.17 ms, i.e. below ~1.3 TB/s of ring bandwidth -- every
 # plausible xGMI figure.  c=8 costs 0.5 ms per layer at TP8 and is not worth it.  (At micro-batch 1
 # the GEMMs are 4x smaller and chunking costs relatively more: profiles/r1_sp_chunks_gemm.jsonl.)
-_DEFAULT_CHUNKS = {2: 4, 4: 4, 8: 4}
+# Round 4, with the two staggered SP halves on the emulated ranks (profiles/r4_emulate_sp_chunks_halves.jsonl):
+# TP8 at 400 GB/s c = 1 / 2 / 4 / 8: 552 / 511 / 517 / 573 ms per step; TP4 at 200 GB/s c = 2 / 4 / 8: 939 / 898 /
+# 923; TP2 at 70 GB/s: 1,843 / 1,753 / 1,830.
+_DEFAULT_CHUNKS = {2: 4, 4: 4, 8: 2}
 
 
 def set_sequence_parallel_chunks(c: Optional[int]) -> None:
