@@ -69,7 +69,7 @@ constexpr int U = 4;   // 512-element k-steps per load round
 // still has thousands of waves streaming.  The first round of weight loads is issued before the
 // RMSNorm prologue: the weights do not depend on the activations.
 template <int MM, int NW, int EPI, bool NORM, int KS>
-__global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
+__device__ __forceinline__ void dgemv_body(const Params& p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* xs = reinterpret_cast<uint16_t*>(smem);   // NORM: [MM][K] normalised bf16 rows
   __shared__ float red[4][MM];
@@ -331,6 +331,20 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
   }
 }
 
+template <int MM, int NW, int EPI, bool NORM, int KS>
+__global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
+  dgemv_body<MM, NW, EPI, NORM, KS>(p);
+}
+
+// The same body capped at 64 VGPRs (8 waves / SIMD).  The bs = 1 two-row kernels need 81-84 VGPRs
+// (5 waves / SIMD = 1,280 resident workgroups), so gate_up's 2,048 workgroups and QKV's 1,536 run
+// as a full round plus a partial one, each paying the HBM latency; at 8 waves / SIMD (2,048 resident)
+// they are one round, for ~100-125 bytes / lane of scratch spills (NXD_DECODE_OCC8, knob 5).
+template <int MM, int NW, int EPI, bool NORM, int KS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) dgemv_kernel_o8(Params p) {
+  dgemv_body<MM, NW, EPI, NORM, KS>(p);
+}
+
 
 // k-slices per row group: split K while the grid stays <= 8192 waves and slices keep >= 1024
 // elements (o_proj 2048 x 2048 -> 2, down 2048 x 8192 -> 4, gate_up / lm_head -> 1)
@@ -338,6 +352,7 @@ int g_glu_pairs = 1;   // knob 0: (gate, up) row pairs per wave of the GLU proje
 int g_ks = 0;          // knob 1: k-slices per row group (0 = pick_ks)
 int g_pf = -1;         // knob 2: early epilogue / prologue reads (Params::pf; NXD_DECODE_EPI_PF, default 1)
 int g_nt = -1;         // knob 3: non-temporal weight loads (Params::nt; NXD_DECODE_NT, default 1)
+int g_occ8 = -1;       // knob 5: bs = 1 two-row kernels at 8 waves / SIMD (dgemv_kernel_o8; NXD_DECODE_OCC8)
 
 // per-projection override (A/B): NXD_DECODE_KS_PLAIN / _RESID / _GLU / _QKV = 1 | 2 | 4
 static int g_ks_epi[4] = {-2, -2, -2, -2};
@@ -363,6 +378,17 @@ static int launch(const Params& p, int groups, hipStream_t s) {
   const size_t lds = NORM ? (size_t)MM * p.K * 2 : 0;
   const int ks = pick_ks(groups, p.K, EPI);
   const dim3 grid((unsigned)((groups * ks + 3) / 4)), block(256);
+  if constexpr (MM == 1 && NW == 2) {
+    if (g_occ8 == 1) {
+      if (ks == 4)
+        hipLaunchKernelGGL((dgemv_kernel_o8<MM, NW, EPI, NORM, 4>), grid, block, lds, s, p);
+      else if (ks == 2)
+        hipLaunchKernelGGL((dgemv_kernel_o8<MM, NW, EPI, NORM, 2>), grid, block, lds, s, p);
+      else
+        hipLaunchKernelGGL((dgemv_kernel_o8<MM, NW, EPI, NORM, 1>), grid, block, lds, s, p);
+      return hipGetLastError() == hipSuccess ? 0 : 1;
+    }
+  }
   if (ks == 4)
     hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 4>), grid, block, lds, s, p);
   else if (ks == 2)
@@ -404,6 +430,7 @@ void dgemv_set_knob(int which, int value) {
   else if (which == 1) dfused::g_ks = value;
   else if (which == 2) dfused::g_pf = value != 0;
   else if (which == 3) dfused::g_nt = value != 0;
+  else if (which == 5) dfused::g_occ8 = value != 0;
 }
 
 int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,
@@ -427,6 +454,10 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
     dfused::g_nt = e ? (atoi(e) != 0) : 1;
   }
   p.nt = dfused::g_nt;
+  if (dfused::g_occ8 < 0) {
+    const char* e = getenv("NXD_DECODE_OCC8");
+    dfused::g_occ8 = e ? (atoi(e) != 0) : 0;
+  }
   const bool norm = norm_w != nullptr;
   if (M == 1) return dfused::dispatch<1>(p, epi, norm, stream);
   if (M == 2) return dfused::dispatch<2>(p, epi, norm, stream);
