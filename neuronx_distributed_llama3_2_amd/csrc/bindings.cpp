@@ -994,11 +994,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("nq"), py::arg("nkv"), py::arg("D"), py::arg("cos_t"), py::arg("sin_t"), py::arg("pos"), py::arg("T"),
         py::arg("kc"), py::arg("vc"), py::arg("cache_idx"), py::arg("xadd") = py::none(), py::arg("yadd") = py::none());
   // decode A/B knobs: 0 = GLU row pairs per wave, 1 = GEMV k-slices (0 auto), 2 = MFMA decode attention on/off,
-  // 3 = GEMV early epilogue / prologue reads on/off, 4 = non-temporal weight loads on/off
+  // 3 = GEMV early epilogue / prologue reads on/off, 5 = bs = 1 GEMV forced occupancy (0 natural | 7 | 8 waves / SIMD)
   m.def("decode_set_knob", [](int which, int value) {
     if (which == 2) nxd::decode_attn_set_v2(value);
     else if (which == 3) nxd::dgemv_set_knob(2, value);
-    else if (which == 4) nxd::dgemv_set_knob(3, value);
     else nxd::dgemv_set_knob(which, value);
   });
   m.doc() = "CDNA4 (gfx950) kernels of neuronx_distributed_llama3_2_amd";

@@ -56,10 +56,6 @@ struct Params {
   int pf;                 // issue the epilogue's / prologue's own global reads (residual row, yadd,
                           // position + cos/sin, RMSNorm weight) at kernel start, next to the first
                           // weight round, instead of as dependent round trips after the GEMV
-  int nt;                 // weight rows loaded non-temporal (global_load ... nt): decode reads every
-                          // weight byte once per token (MI355X_MICROARCH.md, nt-weights).  Llama-3.2-1B
-                          // bs=1: 0.732 -> 0.712 ms/token, alternating A/B on one box
-                          // (profiles/r4_decode_nt_fn_ab.txt)
 };
 
 constexpr int U = 4;   // 512-element k-steps per load round
@@ -74,7 +70,10 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
   uint16_t* xs = reinterpret_cast<uint16_t*>(smem);   // NORM: [MM][K] normalised bf16 rows
   __shared__ float red[4][MM];
   __shared__ float part[4][MM][NW];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // wid is wave-uniform: readfirstlane puts it (and the rows, row pointers and k range derived
+  // from it) in SGPRs, so each weight load is one scalar base + the lane's 16-byte offset + an
+  // immediate, not a 64-bit per-lane address (the VGPR count sets how many waves stream at once)
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int rg = wid / KS, ks = wid % KS;
   const int wave = blockIdx.x * (4 / KS) + rg;          // row-group index
 
@@ -110,55 +109,84 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
 
   const int kc = ((p.K + KS - 1) / KS + 7) & ~7;
   const int kbeg = min(ks * kc, p.K), kend = min(p.K, kbeg + kc);
+  const uint16_t* wrow[NW];
+#pragma unroll
+  for (int r = 0; r < NW; ++r) wrow[r] = p.w + (int64_t)rows[r] * p.ldw;
   u32x4_t wv[NW][U];
+  // Weight rows are loaded non-temporal (global_load ... nt): decode reads every weight byte once per
+  // token (MI355X_MICROARCH.md, nt-weights; Llama-3.2-1B bs=1 0.732 -> 0.712 ms/token,
+  // profiles/r4_decode_nt_fn_ab.txt).  Unpredicated: a lane past kend re-reads the slice's last 16 bytes (in
+  // bounds) and the FMA loop skips it.  Predicated / zero-filled loads or a runtime choice of load
+  // kind made the compiler merge register copies right after the loads, i.e. wait (s_waitcnt
+  // vmcnt) for most of them before the prologue could start, and cost 4-8 VGPRs.
   auto load_round = [&](int base) {
-    if (p.nt) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = base + lane * 8 + u * 512;
+    for (int u = 0; u < U; ++u) {
+      const int k = min(base + u * 512 + lane * 8, kend - 8);
 #pragma unroll
-        for (int r = 0; r < NW; ++r)
-          wv[r][u] = k < kend ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p.w + (int64_t)rows[r] * p.ldw + k))
-                              : u32x4_t{0, 0, 0, 0};
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = base + lane * 8 + u * 512;
-#pragma unroll
-        for (int r = 0; r < NW; ++r)
-          wv[r][u] = k < kend ? *reinterpret_cast<const u32x4_t*>(p.w + (int64_t)rows[r] * p.ldw + k) : u32x4_t{0, 0, 0, 0};
-      }
+      for (int r = 0; r < NW; ++r)
+        wv[r][u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(wrow[r] + k));
     }
   };
+
+  // ---- bs = 1: the RMSNorm prologue's first chunk of x (+ pending xadd, + norm weight) is issued
+  // BEFORE the weight round.  vmcnt retires in issue order, so a load issued after the weights can
+  // only be waited for together with all of them: the prologue then started only once the weights
+  // had landed, and its own L2 round trip and barriers were added to every wave's critical path.
+  // (Left uninitialised where not loaded; only read under the same conditions.)
+  constexpr bool PRE = NORM && MM == 1;
+  u32x4_t x0, gw0 = {0, 0, 0, 0};
+  f32x4_t xa0, xa1;
+  const bool pre_ok = PRE && tid * 8 < p.K;
+  if (pre_ok) {
+    x0 = *reinterpret_cast<const u32x4_t*>(p.x + tid * 8);
+    if (p.xadd) {
+      xa0 = *reinterpret_cast<const f32x4_t*>(p.xadd + tid * 8);
+      xa1 = *reinterpret_cast<const f32x4_t*>(p.xadd + tid * 8 + 4);
+    }
+    gw0 = *reinterpret_cast<const u32x4_t*>(p.norm_w + tid * 8);
+  }
+  // bs = 1 without a norm prologue (down, o_proj): the first round's activation chunks, likewise
+  // ahead of the weights (they were read inside the FMA loop, one L2 round trip after the weights)
+  constexpr bool PREX = !NORM && MM == 1;
+  u32x4_t xv0[PREX ? U : 1];
+  if constexpr (PREX) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) xv0[u] = *reinterpret_cast<const u32x4_t*>(p.x + min(kbeg + u * 512 + lane * 8, kend - 8));
+  }
+  // RESID epilogue operands (p.pf), likewise ahead of the weights and kept raw: converting the bf16
+  // right after its load made the wave wait (vmcnt) there for every weight load issued before it
+  uint16_t y_raw[MM][NW];
+  float ya_pre[MM][NW];
+  if (EPI == RESID && p.pf && lane == 0 && active) {
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int r = 0; r < NW; ++r) {
+        const int n = min(wave * NW + r, p.N - 1);
+        y_raw[m][r] = p.y[(int64_t)m * p.ldy + n];
+        if (p.yadd) ya_pre[m][r] = p.yadd[(int64_t)m * p.N + n];
+      }
+    }
+  }
   load_round(kbeg);
 
   // ---- early epilogue / prologue operands (p.pf): independent of the activations, so their
   // latency overlaps the first weight round instead of following the reduction
-  u32x4_t gw0 = {0, 0, 0, 0};
-  if (NORM && p.pf && tid * 8 < p.K) gw0 = *reinterpret_cast<const u32x4_t*>(p.norm_w + tid * 8);
-  float y_pre[MM][NW], ya_pre[MM][NW];
+  if (!PRE && NORM && p.pf && tid * 8 < p.K) gw0 = *reinterpret_cast<const u32x4_t*>(p.norm_w + tid * 8);
   float cs_pre[MM], sn_pre[MM];
-  if (p.pf && lane == 0 && active) {
+  if (EPI == ROPE_KV && p.pf && lane == 0 && active) {
 #pragma unroll
     for (int m = 0; m < MM; ++m) {
       if (m >= p.M) continue;
-      if (EPI == RESID) {
-#pragma unroll
-        for (int r = 0; r < NW; ++r) {
-          const int n = min(wave * NW + r, p.N - 1);
-          y_pre[m][r] = bf2f(p.y[(int64_t)m * p.ldy + n]);
-          ya_pre[m][r] = p.yadd ? p.yadd[(int64_t)m * p.N + n] : 0.f;
-        }
-      } else if (EPI == ROPE_KV) {
-        const int half = p.D / 2;
-        if (rows[0] < (p.nq + p.nkv) * p.D && rows[1] == rows[0] + half) {
-          const int64_t ps = p.pos[m];
-          const int64_t pt = ps < 0 ? 0 : (ps >= p.max_pos ? p.max_pos - 1 : ps);
-          const int d = rows[0] % p.D;
-          cs_pre[m] = p.cos_t[pt * half + d];
-          sn_pre[m] = p.sin_t[pt * half + d];
-        }
+      const int half = p.D / 2;
+      if (rows[0] < (p.nq + p.nkv) * p.D && rows[1] == rows[0] + half) {
+        const int64_t ps = p.pos[m];
+        const int64_t pt = ps < 0 ? 0 : (ps >= p.max_pos ? p.max_pos - 1 : ps);
+        const int d = rows[0] % p.D;
+        cs_pre[m] = p.cos_t[pt * half + d];
+        sn_pre[m] = p.sin_t[pt * half + d];
       }
     }
   }
@@ -171,12 +199,21 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
 #pragma unroll
       for (int m = 0; m < MM; ++m) {
         if (m < p.M) {
-          u32x4_t v = *reinterpret_cast<const u32x4_t*>(p.x + (int64_t)m * p.ldx + k);
+          u32x4_t v;
+          f32x4_t a0, a1;
+          if (PRE && k == tid * 8) {   // the chunk loaded ahead of the weights
+            v = x0;
+            if (p.xadd) { a0 = xa0; a1 = xa1; }
+          } else {
+            v = *reinterpret_cast<const u32x4_t*>(p.x + (int64_t)m * p.ldx + k);
+            if (p.xadd) {
+              a0 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k);
+              a1 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k + 4);
+            }
+          }
           float f[8];
           unpack8(v, f);
           if (p.xadd) {
-            const f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k);
-            const f32x4_t a1 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k + 4);
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] = bf2f(f2bf(f[j] + bf2f(f2bf(j < 4 ? a0[j] : a1[j - 4]))));
             v = pack8(f);
@@ -198,7 +235,7 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
     for (int m = 0; m < MM; ++m) rstd[m] = rsqrtf((red[0][m] + red[1][m] + red[2][m] + red[3][m]) / (float)p.K + p.eps);
     for (int k = tid * 8; k < p.K; k += 256 * 8) {
       float g[8];
-      unpack8(p.pf && k == tid * 8 ? gw0 : *reinterpret_cast<const u32x4_t*>(p.norm_w + k), g);
+      unpack8((PRE || p.pf) && k == tid * 8 ? gw0 : *reinterpret_cast<const u32x4_t*>(p.norm_w + k), g);
 #pragma unroll
       for (int m = 0; m < MM; ++m) {
         if (m < p.M) {
@@ -219,18 +256,18 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
 #pragma unroll
     for (int r = 0; r < NW; ++r) acc[m][r] = 0.f;
 
-  for (int base = kbeg; base < kend; base += 512 * U) {
-    if (base != kbeg) load_round(base);
+  auto fma_round = [&](int base, bool first) {
+    const bool full = base + 512 * U <= kend;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = base + lane * 8 + u * 512;
-      if (k < kend) {
+      if (full || k < kend) {
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
           if (m < p.M) {
             float xf[8];
-            const uint16_t* xp = NORM ? (xs + m * p.K + k) : (p.x + (int64_t)m * p.ldx + k);
-            unpack8(*reinterpret_cast<const u32x4_t*>(xp), xf);
+            if (PREX && first) unpack8(xv0[PREX ? u : 0], xf);
+            else unpack8(*reinterpret_cast<const u32x4_t*>(NORM ? (xs + m * p.K + k) : (p.x + (int64_t)m * p.ldx + k)), xf);
 #pragma unroll
             for (int r = 0; r < NW; ++r) {
               float wf[8];
@@ -242,6 +279,11 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
         }
       }
     }
+  };
+  if (kbeg < kend) fma_round(kbeg, true);
+  for (int base = kbeg + 512 * U; base < kend; base += 512 * U) {
+    load_round(base);
+    fma_round(base, false);
   }
 #pragma unroll
   for (int m = 0; m < MM; ++m)
@@ -317,7 +359,7 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
         const int n = wave * NW + r;
         if (n >= p.N) continue;
         if (EPI == RESID) {
-          float yv = p.pf ? y_pre[m][r] : bf2f(yr[n]);
+          float yv = p.pf ? bf2f(y_raw[m][r]) : bf2f(yr[n]);
           if (p.yadd) {
             float* ya = p.yadd + (int64_t)m * p.N + n;
             yv = bf2f(f2bf(yv + bf2f(f2bf(p.pf ? ya_pre[m][r] : *ya))));
@@ -336,12 +378,12 @@ __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
   dgemv_body<MM, NW, EPI, NORM, KS>(p);
 }
 
-// The same body capped at 64 VGPRs (8 waves / SIMD).  The bs = 1 two-row kernels need 81-84 VGPRs
-// (5 waves / SIMD = 1,280 resident workgroups), so gate_up's 2,048 workgroups and QKV's 1,536 run
-// as a full round plus a partial one, each paying the HBM latency; at 8 waves / SIMD (2,048 resident)
-// they are one round, for ~100-125 bytes / lane of scratch spills (NXD_DECODE_OCC8, knob 5).
-template <int MM, int NW, int EPI, bool NORM, int KS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) dgemv_kernel_o8(Params p) {
+// The same body at a forced occupancy (WPE waves / SIMD: 7 -> <= 72 VGPRs, 8 -> <= 64).  The bs = 1
+// two-row kernels take 74-76 VGPRs (6 waves / SIMD = 1,536 resident workgroups), so gate_up's
+// 2,048 workgroups run as a full round plus a partial one, each paying the HBM latency.  Forcing 8
+// spills 64-76 bytes / lane and measured 1.17 vs 0.69 ms/token; 7 spills 16-20 (NXD_DECODE_OCC).
+template <int MM, int NW, int EPI, bool NORM, int KS, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) dgemv_kernel_occ(Params p) {
   dgemv_body<MM, NW, EPI, NORM, KS>(p);
 }
 
@@ -351,8 +393,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
 int g_glu_pairs = 1;   // knob 0: (gate, up) row pairs per wave of the GLU projection (1 | 2)
 int g_ks = 0;          // knob 1: k-slices per row group (0 = pick_ks)
 int g_pf = -1;         // knob 2: early epilogue / prologue reads (Params::pf; NXD_DECODE_EPI_PF, default 1)
-int g_nt = -1;         // knob 3: non-temporal weight loads (Params::nt; NXD_DECODE_NT, default 1)
-int g_occ8 = -1;       // knob 5: bs = 1 two-row kernels at 8 waves / SIMD (dgemv_kernel_o8; NXD_DECODE_OCC8)
+int g_occ = -1;        // knob 5: bs = 1 two-row kernels at 7 | 8 waves / SIMD (dgemv_kernel_occ; NXD_DECODE_OCC, 0 = natural)
 
 // per-projection override (A/B): NXD_DECODE_KS_PLAIN / _RESID / _GLU / _QKV = 1 | 2 | 4
 static int g_ks_epi[4] = {-2, -2, -2, -2};
@@ -379,13 +420,16 @@ static int launch(const Params& p, int groups, hipStream_t s) {
   const int ks = pick_ks(groups, p.K, EPI);
   const dim3 grid((unsigned)((groups * ks + 3) / 4)), block(256);
   if constexpr (MM == 1 && NW == 2) {
-    if (g_occ8 == 1) {
-      if (ks == 4)
-        hipLaunchKernelGGL((dgemv_kernel_o8<MM, NW, EPI, NORM, 4>), grid, block, lds, s, p);
-      else if (ks == 2)
-        hipLaunchKernelGGL((dgemv_kernel_o8<MM, NW, EPI, NORM, 2>), grid, block, lds, s, p);
-      else
-        hipLaunchKernelGGL((dgemv_kernel_o8<MM, NW, EPI, NORM, 1>), grid, block, lds, s, p);
+    if (g_occ == 7 || g_occ == 8) {
+#define NXD_OCC_LAUNCH(W)                                                                   \
+  if (ks == 4)                                                                              \
+    hipLaunchKernelGGL((dgemv_kernel_occ<MM, NW, EPI, NORM, 4, W>), grid, block, lds, s, p); \
+  else if (ks == 2)                                                                         \
+    hipLaunchKernelGGL((dgemv_kernel_occ<MM, NW, EPI, NORM, 2, W>), grid, block, lds, s, p); \
+  else                                                                                      \
+    hipLaunchKernelGGL((dgemv_kernel_occ<MM, NW, EPI, NORM, 1, W>), grid, block, lds, s, p);
+      if (g_occ == 7) { NXD_OCC_LAUNCH(7) } else { NXD_OCC_LAUNCH(8) }
+#undef NXD_OCC_LAUNCH
       return hipGetLastError() == hipSuccess ? 0 : 1;
     }
   }
@@ -429,8 +473,7 @@ void dgemv_set_knob(int which, int value) {
   if (which == 0) dfused::g_glu_pairs = value == 2 ? 2 : 1;
   else if (which == 1) dfused::g_ks = value;
   else if (which == 2) dfused::g_pf = value != 0;
-  else if (which == 3) dfused::g_nt = value != 0;
-  else if (which == 5) dfused::g_occ8 = value != 0;
+  else if (which == 5) dfused::g_occ = value;
 }
 
 int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,
@@ -443,20 +486,15 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
   dfused::Params p{static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(norm_w), eps,
                    static_cast<const uint16_t*>(w), ldw, static_cast<uint16_t*>(y), ldy, M, N, K, nq, nkv, D, cos_t,
                    sin_t, pos, T, static_cast<uint16_t*>(kc), static_cast<uint16_t*>(vc), c_sb, c_sh, c_sl, cache_idx,
-                   Lmax, max_pos, xadd, yadd, 1, 1};
+                   Lmax, max_pos, xadd, yadd, 1};
   if (dfused::g_pf < 0) {
     const char* e = getenv("NXD_DECODE_EPI_PF");
     dfused::g_pf = e ? (atoi(e) != 0) : 1;
   }
   p.pf = dfused::g_pf;
-  if (dfused::g_nt < 0) {
-    const char* e = getenv("NXD_DECODE_NT");
-    dfused::g_nt = e ? (atoi(e) != 0) : 1;
-  }
-  p.nt = dfused::g_nt;
-  if (dfused::g_occ8 < 0) {
-    const char* e = getenv("NXD_DECODE_OCC8");
-    dfused::g_occ8 = e ? (atoi(e) != 0) : 0;
+  if (dfused::g_occ < 0) {
+    const char* e = getenv("NXD_DECODE_OCC");
+    dfused::g_occ = e ? atoi(e) : 0;
   }
   const bool norm = norm_w != nullptr;
   if (M == 1) return dfused::dispatch<1>(p, epi, norm, stream);
