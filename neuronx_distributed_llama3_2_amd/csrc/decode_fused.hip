@@ -389,7 +389,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
 
 
 // k-slices per row group: split K while the grid stays <= 8192 waves and slices keep >= 1024
-// elements (o_proj 2048 x 2048 -> 2, down 2048 x 8192 -> 4, gate_up / lm_head -> 1)
+// elements (o_proj 2048 x 2048 -> 2, down 2048 x 8192 -> 4, gate_up / lm_head / QKV -> 1)
 int g_glu_pairs = 1;   // knob 0: (gate, up) row pairs per wave of the GLU projection (1 | 2)
 int g_ks = 0;          // knob 1: k-slices per row group (0 = pick_ks)
 int g_pf = -1;         // knob 2: early epilogue / prologue reads (Params::pf; NXD_DECODE_EPI_PF, default 1)
@@ -409,6 +409,10 @@ static int pick_ks(int groups, int K, int epi) {
   }
   const int f = g_ks_epi[epi & 3];
   if (f == 1 || f == 2 || f == 4) return f;
+  // QKV + RoPE (two rows per wave, K = hidden): whole rows per wave, no LDS partial reduction --
+  // Llama-3.2-1B bs=1 0.6187 / 0.6195 vs 0.6226 / 0.6207 ms/token with 2 slices, alternating
+  // (profiles/r4_decode_shape_sweep.txt)
+  if (epi == ROPE_KV && K <= 4096) return 1;
   int ks = 1;
   while (ks < 4 && groups * ks * 2 <= 8192 && K / (ks * 2) >= 1024) ks *= 2;
   return ks;
@@ -495,6 +499,8 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
   if (dfused::g_occ < 0) {
     const char* e = getenv("NXD_DECODE_OCC");
     dfused::g_occ = e ? atoi(e) : 0;
+    const char* gp = getenv("NXD_DECODE_GLU_PAIRS");
+    if (gp && atoi(gp) == 2) dfused::g_glu_pairs = 2;
   }
   const bool norm = norm_w != nullptr;
   if (M == 1) return dfused::dispatch<1>(p, epi, norm, stream);
