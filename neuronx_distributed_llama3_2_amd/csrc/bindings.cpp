@@ -58,7 +58,7 @@ void decode_attn_set_v2(int);
 void decode_attn_set_prefetch(const void*, int64_t, const void*, int64_t, int);
 int dgemv_launch(int, const void*, int64_t, const void*, float, const void*, int64_t, void*, int64_t, int, int, int, int,
                  int, int, const float*, const float*, const int64_t*, int, void*, void*, int64_t, int64_t, int64_t,
-                 const int*, int, int, const float*, float*, hipStream_t);
+                 const int*, int, int, const float*, float*, hipStream_t, const int64_t*, int64_t, void*);
 int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, int, hipStream_t);
 int wgrad_gemm_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int, int, int, int, hipStream_t);
 int wgrad_gemm_choose_splits(int, int, int);
@@ -855,13 +855,30 @@ void moe_combine_bwd(at::Tensor dout, at::Tensor ys, at::Tensor inv, at::Tensor 
 void dgemv(int64_t epi, at::Tensor x, c10::optional<at::Tensor> norm_w, double eps, at::Tensor w, at::Tensor y,
            int64_t nq, int64_t nkv, int64_t D, c10::optional<at::Tensor> cos_t, c10::optional<at::Tensor> sin_t,
            c10::optional<at::Tensor> pos, int64_t T, c10::optional<at::Tensor> kc, c10::optional<at::Tensor> vc,
-           c10::optional<at::Tensor> cache_idx, c10::optional<at::Tensor> xadd, c10::optional<at::Tensor> yadd) {
+           c10::optional<at::Tensor> cache_idx, c10::optional<at::Tensor> xadd, c10::optional<at::Tensor> yadd,
+           c10::optional<at::Tensor> xidx, c10::optional<at::Tensor> xcopy) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_bf16(y, "y");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "dgemv: x [M, K], w [Nw, K], y [M, N]");
   TORCH_CHECK(x.stride(1) == 1 && w.stride(1) == 1 && y.stride(1) == 1, "dgemv: unit inner strides");
-  const int64_t M = x.size(0), K = x.size(1), N = y.size(1);
+  // xidx (QKV only): x is an embedding table [V, K] and input row m is x[xidx[m]]; xcopy [M, K]
+  // receives the gathered rows (the residual stream)
+  const int64_t M = xidx.has_value() ? xidx->numel() : x.size(0), K = x.size(1), N = y.size(1);
+  const int64_t* xi = nullptr;
+  void* xc = nullptr;
+  if (xidx.has_value()) {
+    TORCH_CHECK(epi == 3 && norm_w.has_value(), "dgemv: xidx needs the QKV epilogue with the RMSNorm prologue");
+    TORCH_CHECK(xidx->scalar_type() == at::kLong && xidx->is_contiguous() && xidx->is_cuda(), "dgemv: int64 xidx [M]");
+    xi = xidx->data_ptr<int64_t>();
+    if (xcopy.has_value()) {
+      check_bf16(*xcopy, "xcopy");
+      TORCH_CHECK(xcopy->is_contiguous() && xcopy->dim() == 2 && xcopy->size(0) == M && xcopy->size(1) == K,
+                  "dgemv: xcopy bf16 contiguous [M, K]");
+      check_aligned16(*xcopy, "xcopy");
+      xc = xcopy->data_ptr();
+    }
+  }
   TORCH_CHECK(M >= 1 && M <= 8 && y.size(0) == M, "dgemv: 1..8 rows");
   TORCH_CHECK(K % 8 == 0 && x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && w.size(1) == K, "dgemv: K / strides");
   check_aligned16(x, "x");
@@ -935,7 +952,7 @@ void dgemv(int64_t epi, at::Tensor x, c10::optional<at::Tensor> norm_w, double e
   }
   check_rc(nxd::dgemv_launch((int)epi, x.data_ptr(), x.stride(0), nw, (float)eps, w.data_ptr(), w.stride(0), y.data_ptr(),
                              y.stride(0), (int)M, (int)N, (int)K, (int)nq, (int)nkv, (int)D, cp, sp, pp, (int)T, kp, vp,
-                             c_sb, c_sh, c_sl, ci, Lmax, max_pos, xa, ya, cur_stream()),
+                             c_sb, c_sh, c_sl, ci, Lmax, max_pos, xa, ya, cur_stream(), xi, x.size(0), xc),
            "dgemv");
 }
 
@@ -992,7 +1009,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_combine_bwd", &moe_combine_bwd);
   m.def("dgemv", &dgemv, py::arg("epi"), py::arg("x"), py::arg("norm_w"), py::arg("eps"), py::arg("w"), py::arg("y"),
         py::arg("nq"), py::arg("nkv"), py::arg("D"), py::arg("cos_t"), py::arg("sin_t"), py::arg("pos"), py::arg("T"),
-        py::arg("kc"), py::arg("vc"), py::arg("cache_idx"), py::arg("xadd") = py::none(), py::arg("yadd") = py::none());
+        py::arg("kc"), py::arg("vc"), py::arg("cache_idx"), py::arg("xadd") = py::none(), py::arg("yadd") = py::none(),
+        py::arg("xidx") = py::none(), py::arg("xcopy") = py::none());
   // decode A/B knobs: 0 = GLU row pairs per wave, 1 = GEMV k-slices (0 auto), 2 = MFMA decode attention on/off,
   // 3 = GEMV early epilogue / prologue reads on/off, 5 = bs = 1 GEMV forced occupancy (0 natural | 7 | 8 waves / SIMD)
   m.def("decode_set_knob", [](int which, int value) {

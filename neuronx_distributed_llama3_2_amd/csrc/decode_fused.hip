@@ -56,6 +56,12 @@ struct Params {
   int pf;                 // issue the epilogue's / prologue's own global reads (residual row, yadd,
                           // position + cos/sin, RMSNorm weight) at kernel start, next to the first
                           // weight round, instead of as dependent round trips after the GEMV
+  // XI kernels (first layer's QKV): x is the embedding table [xrows, K] and row m of the input is
+  // x[xidx[m]] (the embedding gather folded into the prologue); workgroup 0 also stores the gathered
+  // rows to xcopy [M, K] (the residual stream)
+  const int64_t* xidx;
+  int64_t xrows;
+  uint16_t* xcopy;
 };
 
 constexpr int U = 4;   // 512-element k-steps per load round
@@ -64,7 +70,7 @@ constexpr int U = 4;   // 512-element k-steps per load round
 // over KS waves (partials reduced through LDS), so a short-N / long-K projection (o_proj, down)
 // still has thousands of waves streaming.  The first round of weight loads is issued before the
 // RMSNorm prologue: the weights do not depend on the activations.
-template <int MM, int NW, int EPI, bool NORM, int KS>
+template <int MM, int NW, int EPI, bool NORM, int KS, bool XI = false>
 __device__ __forceinline__ void dgemv_body(const Params& p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* xs = reinterpret_cast<uint16_t*>(smem);   // NORM: [MM][K] normalised bf16 rows
@@ -138,7 +144,17 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
   u32x4_t x0, gw0 = {0, 0, 0, 0};
   f32x4_t xa0, xa1;
   const bool pre_ok = PRE && tid * 8 < p.K;
-  if (pre_ok) {
+  // XI: input row m is an embedding-table row picked by a token id (a scalar load); its gather waits
+  // for that id, so it is issued after the weight round instead (below)
+  auto xrow = [&](int m) -> const uint16_t* {
+    if constexpr (XI) {
+      const int64_t t = p.xidx[m];
+      return p.x + (t < 0 ? 0 : (t >= p.xrows ? p.xrows - 1 : t)) * p.ldx;
+    } else {
+      return p.x + (int64_t)m * p.ldx;
+    }
+  };
+  if (!XI && pre_ok) {
     x0 = *reinterpret_cast<const u32x4_t*>(p.x + tid * 8);
     if (p.xadd) {
       xa0 = *reinterpret_cast<const f32x4_t*>(p.xadd + tid * 8);
@@ -171,6 +187,14 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
     }
   }
   load_round(kbeg);
+  if (XI && pre_ok) {
+    x0 = *reinterpret_cast<const u32x4_t*>(xrow(0) + tid * 8);
+    if (p.xadd) {
+      xa0 = *reinterpret_cast<const f32x4_t*>(p.xadd + tid * 8);
+      xa1 = *reinterpret_cast<const f32x4_t*>(p.xadd + tid * 8 + 4);
+    }
+    gw0 = *reinterpret_cast<const u32x4_t*>(p.norm_w + tid * 8);
+  }
 
   // ---- early epilogue / prologue operands (p.pf): independent of the activations, so their
   // latency overlaps the first weight round instead of following the reduction
@@ -205,7 +229,7 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
             v = x0;
             if (p.xadd) { a0 = xa0; a1 = xa1; }
           } else {
-            v = *reinterpret_cast<const u32x4_t*>(p.x + (int64_t)m * p.ldx + k);
+            v = *reinterpret_cast<const u32x4_t*>(xrow(m) + k);
             if (p.xadd) {
               a0 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k);
               a1 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k + 4);
@@ -221,6 +245,7 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) ss[m] += f[j] * f[j];
           *reinterpret_cast<u32x4_t*>(xs + m * p.K + k) = v;
+          if (XI && blockIdx.x == 0 && p.xcopy) *reinterpret_cast<u32x4_t*>(p.xcopy + (int64_t)m * p.K + k) = v;
         }
       }
     }
@@ -373,9 +398,9 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
   }
 }
 
-template <int MM, int NW, int EPI, bool NORM, int KS>
+template <int MM, int NW, int EPI, bool NORM, int KS, bool XI = false>
 __global__ void __launch_bounds__(256) dgemv_kernel(Params p) {
-  dgemv_body<MM, NW, EPI, NORM, KS>(p);
+  dgemv_body<MM, NW, EPI, NORM, KS, XI>(p);
 }
 
 // The same body at a forced occupancy (WPE waves / SIMD: 7 -> <= 72 VGPRs, 8 -> <= 64).  The bs = 1
@@ -418,12 +443,12 @@ static int pick_ks(int groups, int K, int epi) {
   return ks;
 }
 
-template <int MM, int NW, int EPI, bool NORM>
+template <int MM, int NW, int EPI, bool NORM, bool XI = false>
 static int launch(const Params& p, int groups, hipStream_t s) {
   const size_t lds = NORM ? (size_t)MM * p.K * 2 : 0;
   const int ks = pick_ks(groups, p.K, EPI);
   const dim3 grid((unsigned)((groups * ks + 3) / 4)), block(256);
-  if constexpr (MM == 1 && NW == 2) {
+  if constexpr (MM == 1 && NW == 2 && !XI) {
     if (g_occ == 7 || g_occ == 8) {
 #define NXD_OCC_LAUNCH(W)                                                                   \
   if (ks == 4)                                                                              \
@@ -438,11 +463,11 @@ static int launch(const Params& p, int groups, hipStream_t s) {
     }
   }
   if (ks == 4)
-    hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 4>), grid, block, lds, s, p);
+    hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 4, XI>), grid, block, lds, s, p);
   else if (ks == 2)
-    hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 2>), grid, block, lds, s, p);
+    hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 2, XI>), grid, block, lds, s, p);
   else
-    hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 1>), grid, block, lds, s, p);
+    hipLaunchKernelGGL((dgemv_kernel<MM, NW, EPI, NORM, 1, XI>), grid, block, lds, s, p);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -465,6 +490,7 @@ static int dispatch(const Params& p, int epi, bool norm, hipStream_t s) {
       return norm ? launch<MM, 2, GLU, true>(p, p.N, s) : launch<MM, 2, GLU, false>(p, p.N, s);
     case ROPE_KV: {
       const int groups = (p.nq + p.nkv) * (p.D / 2) + (p.nkv * p.D + 1) / 2;
+      if (p.xidx) return norm ? launch<MM, 2, ROPE_KV, true, true>(p, groups, s) : -4;
       return norm ? launch<MM, 2, ROPE_KV, true>(p, groups, s) : launch<MM, 2, ROPE_KV, false>(p, groups, s);
     }
   }
@@ -483,9 +509,11 @@ void dgemv_set_knob(int which, int value) {
 int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,
                  int64_t ldy, int M, int N, int K, int nq, int nkv, int D, const float* cos_t, const float* sin_t,
                  const int64_t* pos, int T, void* kc, void* vc, int64_t c_sb, int64_t c_sh, int64_t c_sl,
-                 const int* cache_idx, int Lmax, int max_pos, const float* xadd, float* yadd, hipStream_t stream) {
+                 const int* cache_idx, int Lmax, int max_pos, const float* xadd, float* yadd, hipStream_t stream,
+                 const int64_t* xidx, int64_t xrows, void* xcopy) {
   if (M < 1 || M > 8 || N < 1 || K < 8 || (K % 8)) return -1;
   if ((xadd && !norm_w) || (yadd && epi != dfused::RESID)) return -3;
+  if (xidx && (epi != dfused::ROPE_KV || !norm_w || xrows < 1)) return -4;
   if (norm_w && (size_t)M * K * 2 > 65536) return -2;
   dfused::Params p{static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(norm_w), eps,
                    static_cast<const uint16_t*>(w), ldw, static_cast<uint16_t*>(y), ldy, M, N, K, nq, nkv, D, cos_t,
@@ -496,6 +524,9 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
     dfused::g_pf = e ? (atoi(e) != 0) : 1;
   }
   p.pf = dfused::g_pf;
+  p.xidx = xidx;
+  p.xrows = xrows;
+  p.xcopy = static_cast<uint16_t*>(xcopy);
   if (dfused::g_occ < 0) {
     const char* e = getenv("NXD_DECODE_OCC");
     dfused::g_occ = e ? atoi(e) : 0;

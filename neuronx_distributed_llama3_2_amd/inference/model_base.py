@@ -44,6 +44,10 @@ _PREFETCH_WGS = int(os.environ.get("NXD_DECODE_PREFETCH_WGS", "256"))
 # from run to run; InferenceConfig(deterministic=True) or NXD_DECODE_ATTN_OPROJ=0 takes the
 # two-launch path (bitwise-reproducible decode, ~5 % slower per token).
 _ATTN_OPROJ = os.environ.get("NXD_DECODE_ATTN_OPROJ", "1") == "1"
+# The token-embedding gather folded into the first layer's QKV launch (its RMSNorm prologue reads the
+# embedding row of each token id and workgroup 0 writes it to the residual stream): one launch less
+# per decode step.  NXD_DECODE_EMB_FUSED=0 keeps the separate embedding kernel (A/B).
+_EMB_FUSED = os.environ.get("NXD_DECODE_EMB_FUSED", "1") == "1"
 
 
 class DecoderInferenceMixin:
@@ -189,16 +193,27 @@ class DecoderInferenceMixin:
         pos = positions.reshape(-1).to(torch.int64).contiguous()
         sid32 = seq_ids.to(torch.int32).contiguous() if seq_ids is not None else None
         emb = self.model.embed_tokens
-        res = ops.vocab_parallel_embedding(input_ids, emb.weight, emb.start_index).reshape(M, -1).contiguous()
+        ew = emb.weight
+        emb_fused = (_EMB_FUSED and emb.start_index == 0 and ew.dtype == torch.bfloat16 and ew.is_contiguous()
+                     and input_ids.dtype == torch.int64)
+        if emb_fused:
+            ids = input_ids.reshape(-1).contiguous()
+            res = torch.empty((M, ew.shape[1]), dtype=ew.dtype, device=ew.device)   # written by layer 0's QKV
+        else:
+            res = ops.vocab_parallel_embedding(input_ids, ew, emb.start_index).reshape(M, -1).contiguous()
         qkv = torch.empty((M, W), dtype=res.dtype, device=res.device)
         for i, layer in enumerate(self.model.layers):
             attn = layer.self_attn
             w_qkv = attn.qkv_proj._fused_weight_bias()[0] if hasattr(attn.qkv_proj, "_fused_weight_bias") \
                 else attn.qkv_proj.weight
             kc, vc = self.kv_cache[i, 0], self.kv_cache[i, 1]
-            # RMSNorm -> QKV -> RoPE -> k/v into the cache, one launch
-            C.dgemv(3, res, layer.input_layernorm.weight, self.eps, w_qkv, qkv, nq, nkv, D, cos_t, sin_t, pos, T,
-                    kc, vc, sid32)
+            # RMSNorm -> QKV -> RoPE -> k/v into the cache, one launch (layer 0: + the embedding gather)
+            if i == 0 and emb_fused:
+                C.dgemv(3, ew, layer.input_layernorm.weight, self.eps, w_qkv, qkv, nq, nkv, D, cos_t, sin_t, pos, T,
+                        kc, vc, sid32, xidx=ids, xcopy=res)
+            else:
+                C.dgemv(3, res, layer.input_layernorm.weight, self.eps, w_qkv, qkv, nq, nkv, D, cos_t, sin_t, pos, T,
+                        kc, vc, sid32)
             q = qkv.view(B, T, nq + 2 * nkv, D)[:, :, :nq]
             ln2, w_gu, w_d = self._fused_ffn_weights(layer)
             if _PREFETCH_MB > 0:

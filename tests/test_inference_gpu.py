@@ -281,6 +281,38 @@ def test_fused_decode_weight_prefetch_is_exact(monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("batch", [1, 2])
+def test_fused_decode_embedding_gather_is_exact(monkeypatch, batch):
+    """The embedding gather folded into layer 0's QKV launch (xidx / xcopy) copies the same bf16
+    rows the embedding kernel would: decode logits and tokens are bit-identical with and without it
+    (bs = 1 takes the prologue-ahead path, bs = 2 the multi-row one)."""
+    from transformers import LlamaConfig, LlamaForCausalLM as HF
+    from neuronx_distributed_llama3_2_amd.inference import model_base
+
+    cfg = LlamaConfig(hidden_size=512, intermediate_size=1024, num_hidden_layers=2, num_attention_heads=8,
+                      num_key_value_heads=2, vocab_size=1000, max_position_embeddings=1024, rms_norm_eps=1e-5,
+                      rope_theta=500000.0, tie_word_embeddings=False, eos_token_id=2)
+    torch.manual_seed(0)
+    sd = {k: v.detach().clone() for k, v in HF(cfg).state_dict().items()}
+    torch.manual_seed(6)
+    ids = torch.randint(3, cfg.vocab_size, (batch, 21))
+    monkeypatch.setattr(model_base, "_ATTN_OPROJ", False)   # deterministic (no fp32 atomics)
+    outs, logits = [], []
+    n = ids.shape[1] + 12
+    last = torch.randint(3, cfg.vocab_size, (batch, 1)).cuda()
+    pos = torch.full((batch, 1), n, dtype=torch.int64, device="cuda")
+    sid = torch.arange(batch, device="cuda")
+    clen = torch.full((batch,), n + 1, dtype=torch.int32, device="cuda")
+    for on in (False, True):
+        monkeypatch.setattr(model_base, "_EMB_FUSED", on)
+        m = _model(cfg, sd, torch.bfloat16, graphs=True, steps=4, device=torch.device("cuda"))
+        outs.append(m.generate(ids, max_new_tokens=12, eos_token_id=-1).cpu())
+        assert m.model._decode_fused_ok is True
+        # one more (eager) decode step on the caches the generation left
+        logits.append(m.model.forward_tokens(last, pos, sid, clen).float().cpu())
+    assert torch.equal(logits[0], logits[1])
+
+
 def test_weight_layout_pass_on_gpu(hf_sd):
     """Measured layout pass at the prefill size: every weight gets a layout, packed copies are
     K-major, and prefill logits match the stored-layout model (forced-packed too)."""
