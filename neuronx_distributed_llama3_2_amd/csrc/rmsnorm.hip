@@ -12,6 +12,8 @@
 // result is bitwise reproducible).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace nxd {
 namespace rms {
 
@@ -60,8 +62,11 @@ __global__ void __launch_bounds__(256) fwd_kernel(const uint16_t* __restrict__ x
   }
 }
 
-// grid-stride over rows; each workgroup accumulates its dw partial in registers.
-template <int VPT>
+// grid-stride over rows; each workgroup accumulates its dw partial in registers.  PIPE: the next
+// row's h / dy / dres vectors are loaded before this row's reduction barrier, so a workgroup's
+// rows no longer pay one HBM round trip each (512 workgroups x 4 waves = 2 waves per SIMD: the
+// per-row latency, not bandwidth, set the time).
+template <int VPT, bool PIPE>
 __global__ void __launch_bounds__(256) bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ h,
                                                   const uint16_t* __restrict__ w, const float* __restrict__ rstd,
                                                   const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
@@ -76,7 +81,25 @@ __global__ void __launch_bounds__(256) bwd_kernel(const uint16_t* __restrict__ d
     for (int j = 0; j < 8; ++j) dwa[i][j] = 0.f;
     if (c < nvec) unpack8(*reinterpret_cast<const u32x4_t*>(w + c * 8), wv[i]);
   }
+  u32x4_t hn[VPT], dn[VPT], rn[VPT];
+  auto load_row = [&](int64_t row) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * blockDim.x;
+      if (c < nvec) {
+        hn[i] = *reinterpret_cast<const u32x4_t*>(h + row * H + c * 8);
+        dn[i] = *reinterpret_cast<const u32x4_t*>(dy + row * H + c * 8);
+        if (dres) rn[i] = *reinterpret_cast<const u32x4_t*>(dres + row * H + c * 8);
+      }
+    }
+  };
+  if (PIPE && (int64_t)blockIdx.x < rows) load_row(blockIdx.x);
   for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    u32x4_t hc[VPT], dc[VPT], rc[VPT];
+    if (!PIPE) load_row(row);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) { hc[i] = hn[i]; dc[i] = dn[i]; rc[i] = rn[i]; }
+    if (PIPE && row + gridDim.x < rows) load_row(row + gridDim.x);
     const float rs = rstd[row];
     float xh[VPT][8], g[VPT][8];
     float dot = 0.f;
@@ -85,8 +108,8 @@ __global__ void __launch_bounds__(256) bwd_kernel(const uint16_t* __restrict__ d
       const int c = threadIdx.x + i * blockDim.x;
       if (c < nvec) {
         float hv[8], dv[8];
-        unpack8(*reinterpret_cast<const u32x4_t*>(h + row * H + c * 8), hv);
-        unpack8(*reinterpret_cast<const u32x4_t*>(dy + row * H + c * 8), dv);
+        unpack8(hc[i], hv);
+        unpack8(dc[i], dv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[i][j] = hv[j] * rs;
@@ -106,7 +129,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(const uint16_t* __restrict__ d
         for (int j = 0; j < 8; ++j) o[j] = rs * (g[i][j] - xh[i][j] * mean);
         if (dres) {
           float rv[8];
-          unpack8(*reinterpret_cast<const u32x4_t*>(dres + row * H + c * 8), rv);
+          unpack8(rc[i], rv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += rv[j];
         }
@@ -179,8 +202,20 @@ int rmsnorm_bwd_launch(const void* dy, const void* h, const void* w, const float
   const int G = rmsnorm_bwd_num_partials(rows);
   if (G == 0) return 0;
   const dim3 grid(G), block(threads);
-#define RMS_BWD(V) hipLaunchKernelGGL(bwd_kernel<V>, grid, block, 0, stream, (const uint16_t*)dy, (const uint16_t*)h, \
-                                      (const uint16_t*)w, rstd, (const uint16_t*)dres, (uint16_t*)dx, dw_part, rows, H)
+  // NXD_RMS_BWD_PIPE=0: the unpipelined loop (A/B; identical results)
+  static const bool pipe = [] {
+    const char* e = getenv("NXD_RMS_BWD_PIPE");
+    return e ? atoi(e) != 0 : true;
+  }();
+#define RMS_BWD(V)                                                                                          \
+  do {                                                                                                      \
+    if (pipe)                                                                                               \
+      hipLaunchKernelGGL((bwd_kernel<V, true>), grid, block, 0, stream, (const uint16_t*)dy, (const uint16_t*)h,  \
+                         (const uint16_t*)w, rstd, (const uint16_t*)dres, (uint16_t*)dx, dw_part, rows, H);       \
+    else                                                                                                    \
+      hipLaunchKernelGGL((bwd_kernel<V, false>), grid, block, 0, stream, (const uint16_t*)dy, (const uint16_t*)h, \
+                         (const uint16_t*)w, rstd, (const uint16_t*)dres, (uint16_t*)dx, dw_part, rows, H);       \
+  } while (0)
   if (vpt <= 1) RMS_BWD(1);
   else if (vpt <= 2) RMS_BWD(2);
   else if (vpt <= 4) RMS_BWD(4);

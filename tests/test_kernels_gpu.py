@@ -169,6 +169,34 @@ def test_rmsnorm(H):
     assert _rel(w.grad, wf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm_bwd_many_rows(with_res):
+    """More rows than backward workgroups (512): every workgroup strides over several rows with the
+    next row's loads in flight (rmsnorm.hip PIPE) -- dx, dres pass-through and dw against fp32."""
+    T, H = 1537, 4096
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True) if with_res else None
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    y, h = ops.rms_norm(x, w, 1e-5, residual=r)
+    xf, wf = x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    rf = r.detach().float().requires_grad_(True) if with_res else None
+    hf = xf + rf if with_res else xf
+    yf = ops.rms_norm_reference(hf, wf, 1e-5)
+    dy = torch.randn_like(y)
+    loss = (y.float() * dy.float()).sum()
+    loss_f = (yf * dy.float()).sum()
+    if with_res:
+        dh = torch.randn_like(h)
+        loss = loss + (h.float() * dh.float()).sum()
+        loss_f = loss_f + (hf * dh.float()).sum()
+    loss.backward()
+    loss_f.backward()
+    assert _rel(x.grad, xf.grad) < 2e-2
+    assert _rel(w.grad, wf.grad) < 2e-2
+    if with_res:
+        assert _rel(r.grad, rf.grad) < 2e-2
+
+
 def test_rope_inplace():
     T, nh, D = 64, 6, 128
     W = nh * D + 256
