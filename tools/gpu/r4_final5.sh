@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-4 check on the final tree (decode GEMV / embedding-gather changes, pipelined RMSNorm
+# backward): GPU suite + smoke + bench, then the rocprof breakdown of one bench step.
+bash tools/gpu/round_check.sh r4f || exit $?
+export TMPDIR=/tmp
+O=gpurun_out/r4f_prof; mkdir -p $O
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O -o run --output-format csv -- python bench.py --steps 1 --warmup 1 > $O/bench.log 2>&1 || exit $?
+T=$(find $O -name "run_kernel_trace.csv" | head -1)
+python tools/step_breakdown.py $T > $O/breakdown.txt && python tools/step_breakdown.py $T --by-kernel > $O/breakdown_by_kernel.txt || exit $?
+rm -f $T
+S=$(find $O -name "run_kernel_stats.csv" | head -1); [ -n "$S" ] && cp $S $O/kernel_stats.csv
+find $O -name "*.csv" ! -name kernel_stats.csv -delete
