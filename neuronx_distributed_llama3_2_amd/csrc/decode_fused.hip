@@ -58,7 +58,8 @@ struct Params {
                           // weight round, instead of as dependent round trips after the GEMV
   // XI kernels (first layer's QKV): x is the embedding table [xrows, K] and row m of the input is
   // x[xidx[m]] (the embedding gather folded into the prologue); workgroup 0 also stores the gathered
-  // rows to xcopy [M, K] (the residual stream)
+  // rows to xcopy [M, K] (the residual stream).  Reference: the separate embed_tokens op ahead of the
+  // first layer (examples/inference/modules/model_base.py:473)
   const int64_t* xidx;
   int64_t xrows;
   uint16_t* xcopy;
