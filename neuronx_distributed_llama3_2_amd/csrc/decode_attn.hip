@@ -82,7 +82,7 @@ __device__ __forceinline__ void prefetch_body(const Params& p, int wg, int nwg) 
 typedef __attribute__((address_space(3))) short4_t lds_s4_t;
 typedef short short8_t __attribute__((ext_vector_type(8)));
 
-template <int D, int NWV, bool FUSE>
+template <int D, int NWV, bool FUSE, bool WO_LATE = true>
 __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
   constexpr int NS = D / 32;      // k-steps of the score MFMA
   constexpr int NDT = D / 16;     // 16-wide d tiles of the output
@@ -104,14 +104,14 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
   const int b = bh / p.Hkv, hkv = bh % p.Hkv;
   const int G = p.Hq / p.Hkv, M = G * p.T;
   // FUSE: this workgroup's Wo block (rows rc * NR .., columns of head group hkv) into registers,
-  // issued before the attention so its HBM latency hides behind it.  Thread (row r0 + pass * RPP,
+  // in flight during the attention so its HBM latency hides behind it.  Thread (row r0 + pass * RPP,
   // 32-column segment seg).
   const int tpr = FUSE ? (G * D) / 32 : 1;
   const int seg = tid % tpr, r0 = tid / tpr, rpp = (64 * NWV) / tpr;
   const int nr = FUSE ? p.Hout / p.R : 0;
   const int row0 = FUSE ? ((int)blockIdx.x % p.R) * nr + r0 : 0;
   u32x4_t wreg[4][4];
-  if constexpr (FUSE) {
+  auto load_wo = [&]() {
     const uint16_t* wb = p.wo + (int64_t)row0 * p.ldwo + (int64_t)hkv * G * D + 32 * seg;
 #pragma unroll
     for (int np = 0; np < 4; ++np) {
@@ -120,7 +120,8 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
         for (int j = 0; j < 4; ++j) wreg[np][j] = *reinterpret_cast<const u32x4_t*>(wb + (int64_t)np * rpp * p.ldwo + 8 * j);
       }
     }
-  }
+  };
+  if constexpr (FUSE && !WO_LATE) load_wo();   // round-3 order (A/B: NXD_DECODE_WO_LATE=0)
   const int cb = p.cache_idx ? p.cache_idx[b] : b;
   const int slen = p.seq_len[b];
   const uint16_t* kbase = p.kc + (int64_t)cb * p.c_sb + (int64_t)hkv * p.c_sh;
@@ -162,6 +163,11 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
   };
   int k0 = split * KPS + wid * KB;
   if (k0 < kend) load_chunk(k0);
+  // FUSE: the Wo block is issued AFTER the q and first K / V loads.  vmcnt retires in issue order:
+  // issued first (round 3), the cold-HBM Wo loads had to land before the first score MFMA could
+  // read its L2-resident K fragments, so their latency was added to the attention instead of
+  // hidden behind it (attention + o_proj 7.16 -> 6.92 us, 0.619 -> 0.614 ms/token alternating, profiles/r4_decode_wo_late_ab.txt).
+  if constexpr (FUSE && WO_LATE) load_wo();
   for (; k0 < kend; k0 += NWV * KB) {
     // ---- scores S^T[key][m] for 4 key tiles of 16
     f32x4_t sc[4];
@@ -410,12 +416,26 @@ int decode_attn_oproj_launch(const void* q, const int64_t* qs, const void* kc, c
   p.attn_wgs = B * Hkv * R;
   const size_t lds = (size_t)nwv * dattn::KB * D * 2 + (size_t)nwv * 16 * D * 4 + (size_t)2 * nwv * 16 * 4;
   const dim3 grid(p.attn_wgs), block(nt);
+  static const bool wo_late = [] {
+    const char* e = getenv("NXD_DECODE_WO_LATE");
+    return e ? atoi(e) != 0 : true;
+  }();
   if (D == 64) {
-    (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<64, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((dattn::attn_kernel<64, 8, true>), grid, block, lds, stream, p);
+    if (wo_late) {
+      (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<64, 8, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((dattn::attn_kernel<64, 8, true, true>), grid, block, lds, stream, p);
+    } else {
+      (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<64, 8, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((dattn::attn_kernel<64, 8, true, false>), grid, block, lds, stream, p);
+    }
   } else {
-    (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<128, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((dattn::attn_kernel<128, 4, true>), grid, block, lds, stream, p);
+    if (wo_late) {
+      (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<128, 4, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((dattn::attn_kernel<128, 4, true, true>), grid, block, lds, stream, p);
+    } else {
+      (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<128, 4, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((dattn::attn_kernel<128, 4, true, false>), grid, block, lds, stream, p);
+    }
   }
   return (int)hipGetLastError();
 }
