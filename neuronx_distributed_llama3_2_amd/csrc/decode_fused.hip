@@ -145,8 +145,10 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
   u32x4_t x0, gw0 = {0, 0, 0, 0};
   f32x4_t xa0, xa1;
   const bool pre_ok = PRE && tid * 8 < p.K;
-  // XI: input row m is an embedding-table row picked by a token id (a scalar load); its gather waits
-  // for that id, so it is issued after the weight round instead (below)
+  // XI: input row m is an embedding-table row picked by a token id (a scalar load).  Its gather is
+  // still issued ahead of the weights: waiting for the id delays the weight round by one scalar
+  // round trip, while a gather issued after the weights made the prologue wait for all of them
+  // (layer-0 QKV 5.89-6.04 vs 5.43-5.45 us for the other layers' launches)
   auto xrow = [&](int m) -> const uint16_t* {
     if constexpr (XI) {
       const int64_t t = p.xidx[m];
@@ -155,8 +157,8 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
       return p.x + (int64_t)m * p.ldx;
     }
   };
-  if (!XI && pre_ok) {
-    x0 = *reinterpret_cast<const u32x4_t*>(p.x + tid * 8);
+  if (pre_ok) {
+    x0 = *reinterpret_cast<const u32x4_t*>(xrow(0) + tid * 8);
     if (p.xadd) {
       xa0 = *reinterpret_cast<const f32x4_t*>(p.xadd + tid * 8);
       xa1 = *reinterpret_cast<const f32x4_t*>(p.xadd + tid * 8 + 4);
@@ -188,14 +190,6 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
     }
   }
   load_round(kbeg);
-  if (XI && pre_ok) {
-    x0 = *reinterpret_cast<const u32x4_t*>(xrow(0) + tid * 8);
-    if (p.xadd) {
-      xa0 = *reinterpret_cast<const f32x4_t*>(p.xadd + tid * 8);
-      xa1 = *reinterpret_cast<const f32x4_t*>(p.xadd + tid * 8 + 4);
-    }
-    gw0 = *reinterpret_cast<const u32x4_t*>(p.norm_w + tid * 8);
-  }
 
   // ---- early epilogue / prologue operands (p.pf): independent of the activations, so their
   // latency overlaps the first weight round instead of following the reduction
