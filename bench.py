@@ -88,30 +88,253 @@ def _free_port() -> int:
     return port
 
 
+# ---- fallback ladder ------------------------------------------------------------------------
+# The first multi-rank RCCL run of this tree is the driver's node run, and a hang or crash in one
+# mode must not cost the whole N-GPU number.  Every rank runs as a child process of a supervisor
+# that never imports torch's GPU side or touches the GPU; if a rung fails (non-zero exit, the
+# child's step watchdog, or the rung's wall budget), every rank's child is killed and all ranks
+# start FRESH children with the next rung's knobs:
+#   1. the defaults (two staggered SP halves on two streams, RCCL channel cap 16, SP chunking);
+#   2. one stream (NXD_SP_STREAMS=1: the one-pass TP + SP step);
+#   3. additionally one SP chunk, RCCL's own channel choice and normal-priority comm streams.
+# The JSON line records the rung that produced it and each failed rung's exit code, reason and
+# stderr tail (the watchdog's stack / flight-recorder dump).
+LADDER = [
+    ("defaults", {}),
+    ("one_stream", {"NXD_SP_STREAMS": "1", "NXD_SP_STREAMS_NO_SP": "0"}),
+    ("conservative", {"NXD_SP_STREAMS": "1", "NXD_SP_STREAMS_NO_SP": "0", "NXD_SP_CHUNKS": "1",
+                      "NXD_RCCL_CHANNELS": "auto", "NXD_COMM_HIGH_PRIORITY": "0"}),
+]
+if os.environ.get("NXD_BENCH_LADDER", "1") == "0":
+    LADDER = LADDER[:1]   # no fallback: the defaults only
+LADDER_BUDGET_S = float(os.environ.get("NXD_BENCH_LADDER_BUDGET_S", "570"))   # inside the driver's 600 s
+LADDER_MIN_RUNG_S = float(os.environ.get("NXD_BENCH_LADDER_MIN_RUNG_S", "120"))  # kept for each later rung
+_PFX = "nxd_ladder/"
+
+
+def _rung_faults(k: int):
+    """Test hook: NXD_BENCH_LADDER_FAULTS="1=site@r#h:hang;2=site@r#h:exit" arms NXD_FAULT_INJECT in
+    rung k only."""
+    for item in filter(None, os.environ.get("NXD_BENCH_LADDER_FAULTS", "").split(";")):
+        rung, spec = item.split("=", 1)
+        if int(rung) == k:
+            return spec
+    return None
+
+
+def _rung_env(base, k: int, knobs):
+    env = dict(base, **knobs, NXD_BENCH_CHILD="1", NXD_BENCH_RUNG=str(k))
+    env.pop("NXD_FAULT_INJECT", None)
+    spec = _rung_faults(k)
+    if spec:
+        env["NXD_FAULT_INJECT"] = spec
+    elif "NXD_FAULT_INJECT" in base and not os.environ.get("NXD_BENCH_LADDER_FAULTS"):
+        env["NXD_FAULT_INJECT"] = base["NXD_FAULT_INJECT"]
+    return env
+
+
+class _Child:
+    """One rank process of a rung: started in its own session (killed as a group), stdout / stderr
+    pumped by threads; JSON result lines held back, the last stderr lines kept for the record."""
+
+    def __init__(self, argv, env, hold_json: bool):
+        import collections
+        import threading
+
+        self.json_lines = []
+        self.tail = collections.deque(maxlen=40)
+        self.p = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, start_new_session=True)
+        self.hold_json = hold_json
+        self.threads = [threading.Thread(target=self._pump, args=(self.p.stdout, sys.stdout, True), daemon=True),
+                        threading.Thread(target=self._pump, args=(self.p.stderr, sys.stderr, False), daemon=True)]
+        for t in self.threads:
+            t.start()
+
+    def _pump(self, src, dst, is_out):
+        for raw in iter(src.readline, b""):
+            line = raw.decode("utf-8", "replace")
+            if is_out and self.hold_json and line.startswith("{") and '"metric"' in line:
+                self.json_lines.append(line.strip())
+                continue
+            if not is_out:
+                self.tail.append(line.rstrip("\n"))
+            dst.write(line)
+            dst.flush()
+
+    def poll(self):
+        return self.p.poll()
+
+    def kill(self):
+        import signal
+
+        if self.p.poll() is None:
+            for sig, wait_s in ((signal.SIGTERM, 5.0), (signal.SIGKILL, 10.0)):
+                try:
+                    os.killpg(self.p.pid, sig)
+                except (ProcessLookupError, PermissionError):
+                    pass
+                try:
+                    self.p.wait(timeout=wait_s)
+                    break
+                except subprocess.TimeoutExpired:
+                    continue
+        self.finish()
+
+    def finish(self):
+        for t in self.threads:
+            t.join(timeout=5.0)
+
+    def tail_text(self, n_chars=1500):
+        return "\n".join(self.tail)[-n_chars:]
+
+
+def _rung_deadline(t_start: float, k: int) -> float:
+    """Wall deadline of rung k (1-based): the budget minus what the later rungs keep in reserve."""
+    return t_start + LADDER_BUDGET_S - (len(LADDER) - k) * LADDER_MIN_RUNG_S
+
+
+def _emit(rec_line: str, k: int, history) -> None:
+    rec = json.loads(rec_line)
+    rec["attempt"] = k
+    rec["ladder_rung"] = LADDER[k - 1][0]
+    rec["ladder_knobs"] = LADDER[k - 1][1]
+    rec["ladder_failed"] = history
+    print(json.dumps(rec), flush=True)
+
+
 def launch_local_ranks(argv, n: int) -> int:
     """`python bench.py --gpus N` without a launcher: start N fresh rank processes (one per GPU,
-    RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set) and wait for them.  The parent never imports torch or
-    touches the GPU and never execs; if one rank fails the others are terminated and the parent
-    exits non-zero with the first failing rank's code."""
-    port = os.environ.get("MASTER_PORT") or str(_free_port())
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
-    rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 128 - code
-                for q in live:
-                    q.terminate()
-        time.sleep(0.2)
+    RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set) per rung of the fallback ladder.  The parent never
+    imports torch or touches the GPU and never execs.  A rung fails when any rank exits non-zero or
+    the rung's wall budget runs out; its ranks are then killed and the next rung starts."""
+    t0 = time.monotonic()
+    history = []
+    rc = 1
+    for k, (name, knobs) in enumerate(LADDER, 1):
+        port = str(_free_port())
+        base = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                    MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        kids = [_Child(argv, _rung_env(dict(base, RANK=str(r), LOCAL_RANK=str(r)), k, knobs), hold_json=(r == 0))
+                for r in range(n)]
+        deadline = _rung_deadline(t0, k)
+        t_rung = time.monotonic()
+        why, rc = None, 0
+        while True:
+            codes = [c.poll() for c in kids]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                rc = c if c > 0 else 128 - c
+                why = f"rank {r} exited {c}"
+                break
+            if codes[0] == 0:
+                break
+            if time.monotonic() > deadline:
+                rc, why = 124, f"rung wall budget ({deadline - t_rung:.0f} s) exhausted"
+                break
+            time.sleep(0.2)
+        if why is None:
+            grace = time.monotonic() + 20.0      # rank 0 is done: the others are in their final barrier
+            while any(c.poll() is None for c in kids) and time.monotonic() < grace:
+                time.sleep(0.2)
+        for c in kids:
+            c.kill()
+        if why is None and kids[0].json_lines:
+            _emit(kids[0].json_lines[-1], k, history)
+            return 0
+        if why is None:
+            rc, why = 1, "rank 0 exited 0 without a result line"
+        tails = {r: c.tail_text() for r, c in enumerate(kids) if c.poll() not in (None, 0)}
+        history.append({"rung": k, "name": name, "knobs": knobs, "rc": rc, "why": why,
+                        "s": round(time.monotonic() - t_rung, 1), "stderr_tail": tails.get(0) or next(iter(tails.values()), "")})
+        sys.stderr.write(f"[bench] ladder rung {k} ({name}) failed: {why}\n")
+        sys.stderr.flush()
+    return rc
+
+
+def supervise_launched_rank(argv) -> int:
+    """Under torch.distributed.run (the driver's N-GPU form): this process is rank RANK's supervisor.
+    It starts the rank as a child per ladder rung and agrees with the other ranks' supervisors over
+    the launcher's TCPStore (host-side only) on the rung's rendezvous port, on failure and on
+    success.  The children rendezvous on their own port with their own store."""
+    from datetime import timedelta
+
+    from torch.distributed import TCPStore
+
+    world = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ["RANK"])
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    mport = int(os.environ["MASTER_PORT"])
+    agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"
+    store = TCPStore(addr, mport, world_size=None if agent else world, is_master=(not agent and rank == 0),
+                     timeout=timedelta(seconds=120), wait_for_workers=False)
+    t0 = time.monotonic()
+    history = []
+    rc = 1
+    for k, (name, knobs) in enumerate(LADDER, 1):
+        key = f"{_PFX}r{k}/"
+        if rank == 0:
+            store.set(key + "port", str(_free_port()))
+        port = store.get(key + "port").decode()
+        env = dict(os.environ, MASTER_PORT=port)
+        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+        child = _Child(argv, _rung_env(env, k, knobs), hold_json=(rank == 0))
+        deadline = _rung_deadline(t0, k)
+        t_rung = time.monotonic()
+        why, rc, done_seen = None, 0, None
+        while True:
+            c = child.poll()
+            if c is not None and c != 0:
+                rc, why = (c if c > 0 else 128 - c), f"rank {rank} exited {c}"
+                store.set(key + "fail", why)
+                break
+            if c == 0:
+                if rank == 0:
+                    break
+                if store.check([_PFX + "done"]):
+                    break
+            if store.check([key + "fail"]):
+                rc, why = 1, "peer: " + store.get(key + "fail").decode()
+                break
+            if rank != 0 and store.check([_PFX + "done"]):
+                done_seen = done_seen or time.monotonic()
+                if time.monotonic() - done_seen > 20.0:
+                    break
+            if time.monotonic() > deadline:
+                rc, why = 124, f"rung wall budget ({deadline - t_rung:.0f} s) exhausted"
+                store.set(key + "fail", f"rank {rank}: {why}")
+                break
+            time.sleep(0.2)
+        if why is None and rank == 0 and not child.json_lines:
+            rc, why = 1, "rank 0 exited 0 without a result line"
+            store.set(key + "fail", why)
+        child.kill()
+        if why is None:
+            if rank == 0:
+                store.set(_PFX + "done", str(k))
+                _emit(child.json_lines[-1], k, history)
+            return 0
+        store.set(key + f"end/{rank}", json.dumps({"rc": rc, "why": why, "tail": child.tail_text()}))
+        # every rank's child of this rung is dead before anyone starts the next rung
+        try:
+            store.wait([key + f"end/{r}" for r in range(world)], timedelta(seconds=60))
+        except Exception:
+            pass
+        ends = {}
+        for r in range(world):
+            try:
+                if store.check([key + f"end/{r}"]):
+                    ends[r] = json.loads(store.get(key + f"end/{r}").decode())
+            except Exception:
+                pass
+        first = next((e for e in ends.values() if not e["why"].startswith("peer:")), ends.get(rank, {}))
+        history.append({"rung": k, "name": name, "knobs": knobs, "rc": first.get("rc", rc),
+                        "why": first.get("why", why), "s": round(time.monotonic() - t_rung, 1),
+                        "stderr_tail": first.get("tail", "")})
+        if rank == 0:
+            sys.stderr.write(f"[bench] ladder rung {k} ({name}) failed: {history[-1]['why']}\n")
+            sys.stderr.flush()
     return rc
 
 
@@ -163,6 +386,34 @@ def _arm_watchdog(rank: int, timeout_s: float):
     return StepWatchdog(timeout_s, on_timeout=dump, exit_on_timeout=True, exit_code=124)
 
 
+def expected_initial_loss(cfg) -> float:
+    """Cross-entropy of the random-init model on random tokens: the final RMSNorm leaves unit-RMS
+    hidden states, so the logits are ~N(0, sigma^2 H) with sigma = initializer_range, and
+    E[logsumexp] = ln V + sigma^2 H / 2 (Llama-3-8B: 11.76 + 0.82 = 12.58; BENCH_r04 loss 12.58)."""
+    import math
+
+    return math.log(cfg.vocab_size) + 0.5 * cfg.initializer_range ** 2 * cfg.hidden_size
+
+
+def _check_initial_loss(loss, cfg, dev) -> float:
+    """Step-0 sanity on every rank, before anything is timed: the loss is finite and within 0.5 of
+    the random-init expectation; otherwise the rung fails (exit 86) instead of timing garbage."""
+    import math
+
+    import torch
+    import torch.distributed as dist
+
+    v = float(loss.item() if torch.is_tensor(loss) else loss)
+    exp = expected_initial_loss(cfg)
+    bad = torch.tensor([0.0 if (math.isfinite(v) and abs(v - exp) <= 0.5) else 1.0], device=dev)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+    if bad.item() > 0:
+        sys.stderr.write(f"[bench] step-0 loss check failed on some rank (this rank: {v}, expected {exp:.3f} +- 0.5)\n")
+        sys.stderr.flush()
+        os._exit(86)
+    return v
+
+
 def main(a):
     import torch
     import torch.distributed as dist
@@ -196,9 +447,12 @@ def main(a):
 
     apply_rccl_env(world_size=world)
     # a failed / timed-out RCCL collective tears the process down (TORCH_NCCL_ASYNC_ERROR_HANDLING)
-    # instead of hanging every rank; the host watchdog below catches what that does not
-    wd_s = float(os.environ.get("NXD_BENCH_WATCHDOG_S", "300"))
-    coll_timeout = configure_collective_watchdog(2 * wd_s)
+    # instead of hanging every rank; the host watchdog below catches what that does not.  The first
+    # optimizer step (startup, GEMM autotuning) gets NXD_BENCH_WATCHDOG_S, every later one
+    # NXD_BENCH_STEP_WATCHDOG_S, so a hang after step 1 leaves the ladder time for its next rungs.
+    wd_s = float(os.environ.get("NXD_BENCH_WATCHDOG_S", "240"))
+    wd_step_s = float(os.environ.get("NXD_BENCH_STEP_WATCHDOG_S", "90"))
+    coll_timeout = configure_collective_watchdog(2 * wd_s if wd_s > 0 else 1800.0)
     dist.init_process_group(backend, rank=rank, world_size=world, timeout=coll_timeout,
                             device_id=torch.device("cuda", local_rank) if use_cuda and backend == "nccl" else None)
     watchdog = _arm_watchdog(rank, wd_s) if wd_s > 0 else None
@@ -279,10 +533,14 @@ def main(a):
         opt.zero_grad()
         return tot / accum   # mean over the step's micro-batches (= the pipeline path's loss)
 
-    for _ in range(a.warmup):
+    loss0 = None
+    for w in range(a.warmup):
         loss = train_step()
         if watchdog is not None:
             watchdog.kick()
+            watchdog.timeout_s = max(wd_step_s, 1.0) if wd_step_s > 0 else watchdog.timeout_s
+        if w == 0:
+            loss0 = _check_initial_loss(loss, cfg, dev)
     if use_cuda:
         torch.cuda.synchronize()
     dist.barrier()
@@ -328,6 +586,7 @@ def main(a):
                        "optimizer": "AdamW fp32-master" + (" ZeRO-1" if dp > 1 else ""),
                        "activation_checkpoint": a.ckpt or "none"},
             "loss": round(float(loss.item() if torch.is_tensor(loss) else loss), 4),
+            "loss_step0": None if loss0 is None else round(loss0, 4),
             "comm_backend": backend,
             "comm_world_size": comm_world,
             "params_per_rank": nparams_local,
@@ -351,6 +610,13 @@ def main(a):
 
 if __name__ == "__main__":
     args = parse()
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_local_ranks(sys.argv[1:], args.gpus))
+    ladder = os.environ.get("NXD_BENCH_LADDER", "1") == "1" and os.environ.get("NXD_BENCH_CHILD") != "1"
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1 or ladder:
+            sys.exit(launch_local_ranks(sys.argv[1:], args.gpus))
+    elif ladder:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']} "
+                             "ranks")
+        sys.exit(supervise_launched_rank(sys.argv[1:]))
     main(args)

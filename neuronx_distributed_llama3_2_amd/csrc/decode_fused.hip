@@ -149,12 +149,23 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
   // still issued ahead of the weights: waiting for the id delays the weight round by one scalar
   // round trip, while a gather issued after the weights made the prologue wait for all of them
   // (layer-0 QKV 5.89-6.04 vs 5.43-5.45 us for the other layers' launches)
+  // An id outside [0, xrows) reads an in-bounds row (clamped address) whose value is then replaced by
+  // zeros at its use (xok), as ops.vocab_parallel_embedding returns a zero row for such ids (pad -1,
+  // another TP rank's vocabulary slice); masking at the use keeps the load ahead of the weights.
   auto xrow = [&](int m) -> const uint16_t* {
     if constexpr (XI) {
       const int64_t t = p.xidx[m];
       return p.x + (t < 0 ? 0 : (t >= p.xrows ? p.xrows - 1 : t)) * p.ldx;
     } else {
       return p.x + (int64_t)m * p.ldx;
+    }
+  };
+  auto xok = [&](int m) -> bool {
+    if constexpr (XI) {
+      const int64_t t = p.xidx[m];
+      return t >= 0 && t < p.xrows;
+    } else {
+      return true;
     }
   };
   if (pre_ok) {
@@ -230,6 +241,7 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
               a1 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k + 4);
             }
           }
+          if (XI && !xok(m)) v = u32x4_t{0u, 0u, 0u, 0u};
           float f[8];
           unpack8(v, f);
           if (p.xadd) {

@@ -280,7 +280,8 @@ class LlamaForCausalLM(nn.Module):
             return 0   # pipeline partitioning traces the one-pass forward
         if not (stream_split.enabled() and self.training and torch.is_grad_enabled() and labels is not None
                 and get_pipeline_model_parallel_size() == 1
-                and (m.sequence_parallel_enabled or stream_split.without_sp())
+                and (m.sequence_parallel_enabled
+                     or (stream_split.without_sp() and get_tensor_model_parallel_size() == 1))
                 and m.activation_checkpoint != "full"
                 and input_ids.dim() == 2 and get_data_parallel_size() == 1):
             return 0

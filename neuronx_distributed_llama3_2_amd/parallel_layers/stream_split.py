@@ -75,7 +75,8 @@ def reserved_cus(n: int, ncu: int = 256) -> List[int]:
 
 def without_sp() -> bool:
     """NXD_SP_STREAMS_NO_SP=1: also split micro-batches that run without sequence parallelism
-    (TP = 1): the parts' kernels then only share the GPU, no collectives to hide (experiment)."""
+    at TP = 1: the parts' kernels then only share the GPU, no collectives to hide.  Only taken at
+    TP = 1 (modeling_llama checks it): TP > 1 without SP keeps the one-pass step."""
     return _NO_SP
 
 

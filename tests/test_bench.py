@@ -86,9 +86,70 @@ def test_bench_hung_rank_exits_through_watchdog():
     env = _env()
     env["NXD_FAULT_INJECT"] = "bench_microstep@1#2:hang"
     env["NXD_BENCH_WATCHDOG_S"] = "20"
+    env["NXD_BENCH_STEP_WATCHDOG_S"] = "20"
+    env["NXD_BENCH_LADDER"] = "0"    # this test: the watchdog exit path of one rung
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 124, (r.returncode, r.stderr[-3000:])
     assert "step watchdog: no progress" in r.stderr
     assert "last collectives issued" in r.stderr and "#" in r.stderr.split("last collectives issued")[1]
     assert not _json_lines(r.stdout)
+
+
+def _ladder_env(**kw):
+    env = _env()
+    # rung 1: rank 1 hangs before its 2nd micro-step (the first timed one) -> step watchdog, exit 124;
+    # rung 2: rank 0 dies at its first micro-step (exit 43); rung 3 must produce the result
+    env["NXD_BENCH_LADDER_FAULTS"] = "1=bench_microstep@1#2:hang;2=bench_microstep@0#1:exit"
+    env["NXD_BENCH_WATCHDOG_S"] = "60"
+    env["NXD_BENCH_STEP_WATCHDOG_S"] = "15"
+    env.update(kw)
+    return env
+
+
+def _check_ladder(r, n, budget_s):
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    _check(rec, n)
+    assert rec["attempt"] == 3 and rec["ladder_rung"] == "conservative"
+    assert rec["ladder_knobs"]["NXD_SP_STREAMS"] == "1" and rec["sp_streams"] == 1
+    failed = rec["ladder_failed"]
+    assert [f["rung"] for f in failed] == [1, 2]
+    assert failed[0]["rc"] == 124 and "last collectives issued" in failed[0]["stderr_tail"], failed[0]
+    assert failed[1]["rc"] == 43 and "injected fault" in failed[1]["stderr_tail"], failed[1]
+    assert sum(f["s"] for f in failed) < budget_s
+    # step-0 sanity: the initial loss is the random-init expectation
+    assert abs(rec["loss_step0"] - math.log(1024)) < 0.5
+
+
+def test_bench_ladder_recovers_self_spawn():
+    """Fallback ladder, no launcher: a hang in rung 1 and a crash in rung 2 still give one valid
+    JSON line from rung 3 (fresh child processes each rung), recording both failures."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=ROOT, env=_ladder_env(),
+                       capture_output=True, text=True, timeout=400)
+    _check_ladder(r, 2, 400)
+
+
+def test_bench_ladder_recovers_under_torchrun():
+    """The same under torch.distributed.run (the driver's N-GPU launch): each launched process is
+    its rank's supervisor; they agree on failure and on each rung's port over the launcher's store."""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29633", "bench.py", "--gpus", "2", *ARGS],
+                       cwd=ROOT, env=_ladder_env(), capture_output=True, text=True, timeout=400)
+    _check_ladder(r, 2, 400)
+
+
+def test_bench_ladder_rung_budget_kills_silent_hang():
+    """With the step watchdog off, a hung rung is ended by its wall budget (the supervisor kills the
+    rank processes) and the next rung still fits in the total budget."""
+    env = _env()
+    env.update(NXD_BENCH_LADDER_FAULTS="1=bench_microstep@1#2:hang", NXD_BENCH_WATCHDOG_S="0",
+               NXD_BENCH_LADDER_BUDGET_S="150", NXD_BENCH_LADDER_MIN_RUNG_S="50")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["attempt"] == 2 and rec["ladder_failed"][0]["rc"] == 124
+    assert "wall budget" in rec["ladder_failed"][0]["why"]

@@ -308,9 +308,15 @@ def test_fused_decode_embedding_gather_is_exact(monkeypatch, batch):
         m = _model(cfg, sd, torch.bfloat16, graphs=True, steps=4, device=torch.device("cuda"))
         outs.append(m.generate(ids, max_new_tokens=12, eos_token_id=-1).cpu())
         assert m.model._decode_fused_ok is True
-        # one more (eager) decode step on the caches the generation left
-        logits.append(m.model.forward_tokens(last, pos, sid, clen).float().cpu())
-    assert torch.equal(logits[0], logits[1])
+        # one more (eager) decode step on the caches the generation left, then the same step with
+        # out-of-range ids (pad -1, past the vocabulary): both paths embed a zero row for those
+        steps = [m.model.forward_tokens(last, pos, sid, clen).float().cpu()]
+        for bad in (-1, cfg.vocab_size + 5):
+            steps.append(m.model.forward_tokens(torch.full_like(last, bad), pos, sid, clen).float().cpu())
+        logits.append(steps)
+    for a, b in zip(logits[0], logits[1]):
+        assert torch.equal(a, b)
+    assert not torch.equal(logits[0][0], logits[0][1])
 
 
 def test_weight_layout_pass_on_gpu(hf_sd):

@@ -8,8 +8,8 @@ bf16 TP=2 and TP=1 round their partial sums differently (the row-parallel all-re
 partials), so a random-init model can flip a greedy argmax where its top-2 logits nearly tie.  The
 check: greedy tokens identical for all 64 new tokens -- or, at the first differing position,
 teacher-forced prefill logits of both servers agree (relative L2 error <= 2e-2, relative max error
-<= 6e-2) and the TP=1
-top-2 margin there is within the measured TP=1 / TP=2 logit difference (a genuine near-tie).  The
+<= 3.5e-2) and, in each row that flips, TP=1's margin between its token and TP=2's token is within
+the two servers' logit differences at those two tokens (a genuine near-tie).  The
 "peaked" model (untied lm_head = a row permutation of the embedding: next token = pi(current) by a
 wide margin) must match exactly."""
 
@@ -96,12 +96,23 @@ def test_tp2_server_greedy_matches_tp1_on_gpu(kind):
         lb = servers[2].pool.call("_context_encode", prefix).float()
         # bf16 TP=1 (fused decode kernels) vs TP=2 (unfused, all-reduced partials) over 16 layers:
         # the whole logit vector agrees to ~1 % (L2), single logits to a few % of the largest
+        if la.dim() == 3:
+            la, lb = la[:, -1], lb[:, -1]
         rel_l2 = (la - lb).norm() / la.norm()
         rel_max = (la - lb).abs().max() / la.abs().max()
-        assert rel_l2 <= 2e-2 and rel_max <= 6e-2, (float(rel_l2), float(rel_max))
-        top2 = la.topk(2, dim=-1).values
-        margin = (top2[:, 0] - top2[:, 1]).min()
-        assert margin <= 2 * (la - lb).abs().max(), (diff, float(margin), float((la - lb).abs().max()))
+        # measured worst case 2.79e-2 (profiles/r4b_gpu_tests_spmd_flake.log); a small margin above it
+        assert rel_l2 <= 2e-2 and rel_max <= 3.5e-2, (float(rel_l2), float(rel_max))
+        # near-tie where the tokens differ: TP=1's preference for its token i1 over TP=2's token i2
+        # must be within the two servers' logit differences AT THOSE TWO TOKENS (not over the vocab)
+        margin = torch.tensor(0.0)
+        for r in (a[:, diff] != b[:, diff]).nonzero().flatten().tolist():
+            i1, i2 = int(a[r, diff]), int(b[r, diff])
+            m = la[r, i1] - la[r, i2]
+            slack = (la[r, i1] - lb[r, i1]).abs() + (la[r, i2] - lb[r, i2]).abs()
+            # |m|: the tokens came from the decode kernels, la from the prefill ones (either may
+            # rank the pair the other way inside the same noise)
+            assert m.abs() <= slack, (diff, r, float(m), float(slack))
+            margin = torch.maximum(margin, m.abs().cpu())
         print(f"{kind}: identical for {diff - 16} new tokens, then a near-tie (margin {float(margin):.4f})")
     finally:
         for s in servers.values():
