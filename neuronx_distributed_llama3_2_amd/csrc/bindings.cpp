@@ -21,6 +21,7 @@ int flash_attn_bwd_launch(const void*, const void*, const void*, const void*, co
                           float, int, int, const DropoutArgs&, hipStream_t);
 int rmsnorm_fwd_launch(const void*, const void*, const void*, void*, void*, float*, int64_t, int, float, hipStream_t);
 int rmsnorm_bwd_num_partials(int64_t);
+void rmsnorm_set_rows_path(int);
 int rmsnorm_bwd_launch(const void*, const void*, const void*, const float*, const void*, void*, float*, float*, int,
                        int64_t, int, hipStream_t);
 int rope_inplace_launch(void*, int64_t, int64_t, int, int, int, const float*, const float*, const int64_t*, int64_t,
@@ -1029,6 +1030,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("flash_attn_set_knob", [](int which, int value) { nxd::flash_attn_bwd_set_knob(which, value); });
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rmsnorm_set_rows_path", [](bool on) { nxd::rmsnorm_set_rows_path(on ? 1 : 0); });
   m.def("rope_inplace", &rope_inplace);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("transpose_bf16", &transpose_bf16);

@@ -12,6 +12,7 @@
 // result is bitwise reproducible).
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace nxd {
@@ -168,12 +169,207 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ p
   }
 }
 
+// ---- row-per-wave kernels (H a multiple of 512, H <= 4096: every Llama width up to 8B) ---------
+// One wave owns one row at a time: lane l holds the 16-byte vectors l, l+64, ... (VPL = H / 512 of
+// them, each wave-instruction one contiguous KiB), so the row's sum of squares / dot product is a
+// wave reduction with no barrier, and a wave's next row is independent of its neighbours'.  The
+// one-row-per-workgroup kernels above paid two block barriers per row and kept little in flight:
+// the backward measured 1.98 TB/s at 8192 x 4096 (profiles/r4_rmsnorm_bwd_pipe_ab.txt), and its
+// 128-workgroup column sum of 512 per-workgroup partials was latency-bound beside concurrent work.
+template <int VPL, bool RES>
+__global__ void __launch_bounds__(256) fwd_rows_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+                                                       const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                                                       uint16_t* __restrict__ h_out, float* __restrict__ rstd_out,
+                                                       int64_t rows, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  u32x4_t wv[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) wv[i] = *reinterpret_cast<const u32x4_t*>(w + (i * 64 + lane) * 8);
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += wstride) {
+    const uint16_t* xr = x + row * H + lane * 8;
+    u32x4_t xv[VPL], rv[VPL];
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      xv[i] = *reinterpret_cast<const u32x4_t*>(xr + i * 512);
+      if (RES) rv[i] = *reinterpret_cast<const u32x4_t*>(res + row * H + lane * 8 + i * 512);
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      float v[8];
+      unpack8(xv[i], v);
+      if (RES) {
+        float r[8];
+        unpack8(rv[i], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j] + r[j]));   // round like the stored h
+        xv[i] = pack8(v);
+        *reinterpret_cast<u32x4_t*>(h_out + row * H + lane * 8 + i * 512) = xv[i];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)H + eps);
+    if (lane == 0 && rstd_out) rstd_out[row] = rstd;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      float v[8], g[8];
+      unpack8(xv[i], v);
+      unpack8(wv[i], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = v[j] * rstd * g[j];
+      *reinterpret_cast<u32x4_t*>(y + row * H + lane * 8 + i * 512) = pack8(v);
+    }
+  }
+}
+
+// 8 waves per workgroup, one workgroup per CU (G <= 256 workgroups, grid-stride over rows); each lane
+// accumulates dw for its 8 * VPL columns in registers over all of its wave's rows; the 8 waves' sums
+// are added through LDS (fixed order) into ONE partial row per workgroup, so the column sum reads
+// G <= 256 rows instead of 512.  Bitwise reproducible (no atomics, fixed row -> wave assignment).
+template <int VPL, bool RES>
+__global__ void __launch_bounds__(512) bwd_rows_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ h,
+                                                       const uint16_t* __restrict__ w, const float* __restrict__ rstd,
+                                                       const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
+                                                       float* __restrict__ dw_part, int64_t rows, int H) {
+  __shared__ float red[8][520];   // one 512-column slice of the 8 waves' dw sums (+8 pad)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t wstride = (int64_t)gridDim.x * 8;
+  u32x4_t wv[VPL];
+  float dwa[VPL][8];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    wv[i] = *reinterpret_cast<const u32x4_t*>(w + (i * 64 + lane) * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dwa[i][j] = 0.f;
+  }
+  for (int64_t row = (int64_t)blockIdx.x * 8 + wave; row < rows; row += wstride) {
+    const int64_t off = row * H + lane * 8;
+    u32x4_t hv[VPL], dv[VPL], rv[VPL];
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      hv[i] = *reinterpret_cast<const u32x4_t*>(h + off + i * 512);
+      dv[i] = *reinterpret_cast<const u32x4_t*>(dy + off + i * 512);
+      if (RES) rv[i] = *reinterpret_cast<const u32x4_t*>(dres + off + i * 512);
+    }
+    const float rs = rstd[row];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      float a[8], d[8], g[8];
+      unpack8(hv[i], a);
+      unpack8(dv[i], d);
+      unpack8(wv[i], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = a[j] * rs;
+        dot += d[j] * g[j] * xh;
+        dwa[i][j] += d[j] * xh;
+      }
+    }
+    const float mean = wave_sum(dot) / (float)H;
+    // re-unpack from the packed registers below instead of keeping the first pass's 3 x 8 x VPL
+    // unpacked floats alive (at VPL = 8 that spilled ~100 VGPRs)
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) asm volatile("" : "+v"(hv[i]), "+v"(dv[i]), "+v"(wv[i]));
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      float a[8], d[8], g[8], o[8];
+      unpack8(hv[i], a);
+      unpack8(dv[i], d);
+      unpack8(wv[i], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = rs * (d[j] * g[j] - a[j] * rs * mean);
+      if (RES) {
+        float r[8];
+        unpack8(rv[i], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += r[j];
+      }
+      *reinterpret_cast<u32x4_t*>(dx + off + i * 512) = pack8(o);
+    }
+  }
+  // workgroup partial: slice i (columns [512 i, 512 i + 512)) of the 8 waves' sums, in wave order
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = dwa[i][j];
+    __syncthreads();
+    const int c = threadIdx.x;   // 512 threads = the slice's 512 columns
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += red[q][c];
+    dw_part[(int64_t)blockIdx.x * H + i * 512 + c] = t;
+  }
+}
+
+// dw[c] (+)= sum_g part[g][c] over G <= 256 partial rows: 64 columns per workgroup, 16 row lanes x 16
+// float4 column quads, every row load of a thread in flight at once (G / 16 <= 16), then a fixed-order
+// LDS sum of the 16 row lanes.
+__global__ void __launch_bounds__(256) colsum4_kernel(const float* __restrict__ part, float* __restrict__ out, int G,
+                                                      int H, int accumulate) {
+  __shared__ f32x4_t red[16][17];
+  const int q = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + q * 4;
+  f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+  if (c < H) {
+#pragma unroll 16
+    for (int g = rl; g < G; g += 16) s += *reinterpret_cast<const f32x4_t*>(part + (int64_t)g * H + c);
+  }
+  red[rl][q] = s;
+  __syncthreads();
+  if (rl == 0 && c < H) {
+    f32x4_t t = red[0][q];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) t += red[i][q];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[c + j] = accumulate ? out[c + j] + t[j] : t[j];   // out: any 4-B alignment
+  }
+}
+
+// NXD_RMS_ROWS=0 (or rmsnorm_set_rows_path(0)): the one-row-per-workgroup kernels (A/B)
+static int g_rows_mode = -1;
+static bool rows_path(int H) {
+  if (g_rows_mode < 0) {
+    const char* e = getenv("NXD_RMS_ROWS");
+    g_rows_mode = e ? (atoi(e) != 0) : 1;
+  }
+  return g_rows_mode && H % 512 == 0 && H >= 512 && H <= 4096;
+}
+
 }  // namespace rms
 
 int rmsnorm_fwd_launch(const void* x, const void* res, const void* w, void* y, void* h_out, float* rstd, int64_t rows,
                        int H, float eps, hipStream_t stream) {
   using namespace rms;
   if (H % 8 != 0) return -1;
+  if (rows_path(H)) {
+    if (rows == 0) return 0;
+    const int g = (int)std::min<int64_t>(ceil_div64(rows, 4), 2048);
+#define RMS_FWD_ROWS(V)                                                                                        \
+  do {                                                                                                         \
+    if (res)                                                                                                   \
+      hipLaunchKernelGGL((fwd_rows_kernel<V, true>), dim3(g), dim3(256), 0, stream, (const uint16_t*)x,         \
+                         (const uint16_t*)res, (const uint16_t*)w, (uint16_t*)y, (uint16_t*)h_out, rstd, rows, H, eps); \
+    else                                                                                                       \
+      hipLaunchKernelGGL((fwd_rows_kernel<V, false>), dim3(g), dim3(256), 0, stream, (const uint16_t*)x,        \
+                         (const uint16_t*)res, (const uint16_t*)w, (uint16_t*)y, (uint16_t*)h_out, rstd, rows, H, eps); \
+  } while (0)
+    switch (H / 512) {
+      case 1: RMS_FWD_ROWS(1); break;
+      case 2: RMS_FWD_ROWS(2); break;
+      case 3: RMS_FWD_ROWS(3); break;
+      case 4: RMS_FWD_ROWS(4); break;
+      case 5: RMS_FWD_ROWS(5); break;
+      case 6: RMS_FWD_ROWS(6); break;
+      case 7: RMS_FWD_ROWS(7); break;
+      default: RMS_FWD_ROWS(8); break;
+    }
+#undef RMS_FWD_ROWS
+    return (int)hipGetLastError();
+  }
   const int nvec = H / 8;
   const int threads = nvec >= 256 ? 256 : ((nvec + 63) / 64) * 64;
   const int vpt = (nvec + threads - 1) / threads;
@@ -189,6 +385,8 @@ int rmsnorm_fwd_launch(const void* x, const void* res, const void* w, void* y, v
   return (int)hipGetLastError();
 }
 
+void rmsnorm_set_rows_path(int on) { rms::g_rows_mode = on ? 1 : 0; }
+
 // dw_part must hold G*H floats where G = rmsnorm_bwd_num_partials(rows)
 int rmsnorm_bwd_num_partials(int64_t rows) { return (int)(rows < 512 ? rows : 512); }
 
@@ -196,6 +394,35 @@ int rmsnorm_bwd_launch(const void* dy, const void* h, const void* w, const float
                        float* dw_part, float* dw, int accumulate_dw, int64_t rows, int H, hipStream_t stream) {
   using namespace rms;
   if (H % 8 != 0) return -1;
+  if (rows_path(H)) {
+    // G <= 256 <= rmsnorm_bwd_num_partials(rows) for rows >= 256 (and ceil(rows / 8) <= rows below)
+    const int G = (int)std::min<int64_t>(ceil_div64(rows, 8), 256);
+    if (G == 0) return 0;
+#define RMS_BWD_ROWS(V)                                                                                        \
+  do {                                                                                                         \
+    if (dres)                                                                                                  \
+      hipLaunchKernelGGL((bwd_rows_kernel<V, true>), dim3(G), dim3(512), 0, stream, (const uint16_t*)dy,        \
+                         (const uint16_t*)h, (const uint16_t*)w, rstd, (const uint16_t*)dres, (uint16_t*)dx, dw_part, \
+                         rows, H);                                                                             \
+    else                                                                                                       \
+      hipLaunchKernelGGL((bwd_rows_kernel<V, false>), dim3(G), dim3(512), 0, stream, (const uint16_t*)dy,       \
+                         (const uint16_t*)h, (const uint16_t*)w, rstd, (const uint16_t*)dres, (uint16_t*)dx, dw_part, \
+                         rows, H);                                                                             \
+  } while (0)
+    switch (H / 512) {
+      case 1: RMS_BWD_ROWS(1); break;
+      case 2: RMS_BWD_ROWS(2); break;
+      case 3: RMS_BWD_ROWS(3); break;
+      case 4: RMS_BWD_ROWS(4); break;
+      case 5: RMS_BWD_ROWS(5); break;
+      case 6: RMS_BWD_ROWS(6); break;
+      case 7: RMS_BWD_ROWS(7); break;
+      default: RMS_BWD_ROWS(8); break;
+    }
+#undef RMS_BWD_ROWS
+    hipLaunchKernelGGL(colsum4_kernel, dim3((H + 63) / 64), dim3(256), 0, stream, dw_part, dw, G, H, accumulate_dw);
+    return (int)hipGetLastError();
+  }
   const int nvec = H / 8;
   const int threads = nvec >= 256 ? 256 : ((nvec + 63) / 64) * 64;
   const int vpt = (nvec + threads - 1) / threads;

@@ -574,3 +574,41 @@ def test_adamw_stochastic_rounding_matches_reference():
                     1e-12, 0.9, 0.95, 1e-8, 0.0, 1, sr_seed=12345)
     err = (q16.float() - q).mean().item()
     assert abs(err) < 1e-4, err
+
+
+@pytest.mark.parametrize("H", [512, 1536, 3072, 4096])
+@pytest.mark.parametrize("T", [1, 9, 2049, 5003])
+def test_rmsnorm_rows_path_vs_fp32(H, T):
+    """Row-per-wave RMSNorm kernels (H % 512 == 0, H <= 4096; csrc/rmsnorm.hip fwd_rows / bwd_rows /
+    colsum4): rows below and above the grid's 8 x 256 rows per round (grid-stride), residual fused,
+    dw accumulated into a nonzero fp32 main_grad -- against fp32 torch, and against the one-row-per-
+    workgroup kernels."""
+    from neuronx_distributed_llama3_2_amd import _C
+
+    g = torch.Generator(device=DEV).manual_seed(T * 7 + H)
+    x, r, dy, dres = (torch.randn(T, H, device=DEV, generator=g).to(torch.bfloat16) for _ in range(4))
+    w = (1 + 0.1 * torch.randn(H, device=DEV, generator=g)).to(torch.bfloat16)
+    mg0 = torch.randn(H, device=DEV, generator=g)
+    outs = {}
+    try:
+        for path in (True, False):
+            _C.rmsnorm_set_rows_path(path)
+            y, h, rstd = torch.empty_like(x), torch.empty_like(x), torch.empty(T, device=DEV)
+            _C.rmsnorm_fwd(x, r, w, y, h, rstd, 1e-5)
+            dx, mg = torch.empty_like(x), mg0.clone()
+            _C.rmsnorm_bwd(dy, h, w, rstd, dres, dx, mg, True)
+            outs[path] = (y, h, rstd, dx, mg)
+    finally:
+        _C.rmsnorm_set_rows_path(True)
+    y, h, rstd, dx, mg = outs[True]
+    hf = h.float().requires_grad_(True)   # the stored (bf16-rounded) h is what the backward reads
+    wf = w.float().requires_grad_(True)
+    yf = ops.rms_norm_reference(hf, wf, 1e-5)
+    yf.backward(dy.float())
+    assert torch.equal(h, (x.float() + r.float()).to(torch.bfloat16))
+    assert _rel(y, yf) < 1e-2
+    assert _rel(rstd, torch.rsqrt(h.float().pow(2).mean(-1) + 1e-5)) < 1e-5
+    assert _rel(dx, hf.grad + dres.float()) < 2e-2
+    assert _rel(mg - mg0, wf.grad) < 1e-3
+    for a, b in zip(outs[True], outs[False]):
+        assert _rel(a, b) < 1e-2
