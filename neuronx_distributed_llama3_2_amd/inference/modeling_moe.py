@@ -12,8 +12,8 @@ the down projection, like a dense MLP):
   its epilogue; static shapes, no host sync, captured in the decode hipGraph;
 * small T under graph capture (batched decode / speculation) — every token through every expert
   as two batched GEMMs (each expert's weights read once, static shapes);
-* prefill — tokens sorted by expert, each expert multiplies only its own rows (grouped GEMMs,
-  top_k / E of the dense work; eager, one host sync for the group sizes).
+* prefill — tokens sorted by expert on the device, each expert multiplies only its own rows (the
+  training path's grouped GEMM kernels, top_k / E of the dense work, no host sync).
 
 To feed the skinny-GEMM kernel, the expert weights are stored output-major ([E, out, in] in
 memory) while keeping their logical [E, in, out] parameter shapes (`post_load`).
@@ -30,7 +30,9 @@ import torch
 import torch.nn.functional as F
 
 from ..models.mixtral.modeling_mixtral import MixtralForCausalLM
+from ..ops._ext import ext, use_native
 from ..ops.gemv import expert_linear
+from ..ops.grouped_gemm import moe_dispatch, moe_permutation, moe_unpermute_combine
 from ..ops import swiglu
 from .model_base import DecoderInferenceMixin
 
@@ -117,6 +119,16 @@ class MoEInferenceModel(DecoderInferenceMixin, MixtralForCausalLM):
         return torch.einsum("enh,ne->nh", y.float(), dense_w).to(x.dtype)
 
     def _grouped(self, x, top_w, top_i, w_gu, w_d):
+        """Prefill: (token, choice) slots sorted by expert on the device, each expert multiplying only
+        its own rows.  GPU bf16: the training path's sync-free kernels -- device-side permutation,
+        dispatch gather, the grouped GEMMs (csrc/grouped_rowgemm.hip / grouped_gemm.hip) with the
+        expert weights read output-major in place, SwiGLU, and the fused un-permute + affinity
+        combine (csrc/moe_combine.hip); no host read of the group sizes, so a prefill graph can
+        capture it.  Otherwise (CPU, fp32): per-expert matmuls over host-read group sizes.
+        Reference: src/neuronx_distributed/modules/moe/expert_mlps.py:169-265."""
+        if x.is_cuda and x.dtype == torch.bfloat16 and use_native(x) and x.shape[1] % 8 == 0 \
+                and w_gu.shape[2] % 8 == 0 and top_i.shape[1] <= 8:
+            return self._grouped_device(x, top_w, top_i, w_gu, w_d)
         n, k = top_i.shape
         flat = top_i.reshape(-1)
         order = torch.argsort(flat, stable=True)
@@ -135,3 +147,22 @@ class MoEInferenceModel(DecoderInferenceMixin, MixtralForCausalLM):
         out.index_add_(0, tok, ys)
         return out.to(x.dtype)
 
+    def _grouped_device(self, x, top_w, top_i, w_gu, w_d):
+        n, k = top_i.shape
+        order, inverse, offs = moe_permutation(top_i, self.num_experts)
+        xs = moe_dispatch(x, order, inverse, k)                       # [n*k, H], expert-sorted rows
+        gu = _grouped_mm(xs, w_gu, offs)                              # [n*k, 2I/tp]
+        ys = _grouped_mm(swiglu(gu), w_d, offs)                       # [n*k, H] partial over TP
+        return moe_unpermute_combine(ys, inverse, top_w.float())      # [n, H]
+
+
+def _grouped_mm(x: torch.Tensor, w: torch.Tensor, offs: torch.Tensor) -> torch.Tensor:
+    """y[rows of e] = x[rows of e] @ w[e] for logical w [E, K, N], read in its stored layout: the
+    grouped kernel's forward mode for [E, K, N]-contiguous weights, its input-gradient mode (x @ W^T)
+    for the output-major [E, N, K] storage `post_load` gives the expert weights."""
+    y = torch.empty(x.shape[0], w.shape[2], dtype=x.dtype, device=x.device)
+    if w.is_contiguous():
+        ext().grouped_gemm(0, x.contiguous(), w, offs, y, False)
+    else:
+        ext().grouped_gemm(1, x.contiguous(), w.transpose(1, 2).contiguous(), offs, y, False)
+    return y

@@ -8,9 +8,12 @@ export PYTHONUNBUFFERED=1
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   tests/test_kernels_gpu.py -k "rmsnorm" \
   tests/test_inference_gpu.py -k "embedding_gather" \
-  tests/test_gemm_exhaustive_gpu.py > gpurun_out/r5a/pytest.log 2>&1 || { tail -30 gpurun_out/r5a/pytest.log; exit 1; }
+  tests/test_gemm_exhaustive_gpu.py tests/test_moe_gpu.py > gpurun_out/r5a/pytest.log 2>&1 || { tail -30 gpurun_out/r5a/pytest.log; exit 1; }
 tail -3 gpurun_out/r5a/pytest.log
 timeout -k 10 300 python -u tools/bench_rmsnorm.py > gpurun_out/r5a/rmsnorm_ab.jsonl 2>gpurun_out/r5a/rmsnorm_ab.err || exit 1
 cat gpurun_out/r5a/rmsnorm_ab.jsonl
 timeout -k 10 400 python -u bench.py --steps 6 --warmup 2 > gpurun_out/r5a/bench.json 2> gpurun_out/r5a/bench.err || { tail -30 gpurun_out/r5a/bench.err; exit 1; }
 cat gpurun_out/r5a/bench.json
+timeout -k 10 1000 python -u -m pytest -x -v -s --timeout 900 --timeout-method thread tests/test_convergence_gpu.py \
+  > gpurun_out/r5a/convergence.log 2>&1 || { tail -30 gpurun_out/r5a/convergence.log; exit 1; }
+grep -E "within rtol|passed|failed" gpurun_out/r5a/convergence.log
