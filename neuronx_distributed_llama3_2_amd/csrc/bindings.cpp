@@ -8,6 +8,11 @@
 
 #include "common.h"
 
+#include <execinfo.h>
+#include <csignal>
+#include <cstdlib>
+#include <unistd.h>
+
 namespace nxd {
 int flash_attn_fwd_launch(const void*, const void*, const void*, void*, float*, const int64_t*, const int64_t*,
                           const int64_t*, const int64_t*, int, int, int, int, int, int, float, int, int,
@@ -57,6 +62,7 @@ int expert_gemv_launch(const void*, int64_t, const void*, int64_t, int64_t, cons
 void dgemv_set_knob(int, int);
 void decode_attn_set_v2(int);
 void decode_attn_set_prefetch(const void*, int64_t, const void*, int64_t, int);
+void decode_attn_set_trace(uint64_t*);
 int dgemv_launch(int, const void*, int64_t, const void*, float, const void*, int64_t, void*, int64_t, int, int, int, int,
                  int, int, const float*, const float*, const int64_t*, int, void*, void*, int64_t, int64_t, int64_t,
                  const int*, int, int, const float*, float*, hipStream_t, const int64_t*, int64_t, void*);
@@ -963,7 +969,42 @@ void register_gemm(pybind11::module& m);  // gemm.cpp
 void register_dataloader(pybind11::module& m);  // dataloader.cpp
 void register_comm(pybind11::module& m);  // comm.cpp
 
+// SIGABRT: print the native stack (backtrace_symbols_fd writes straight to fd 2, no allocation) and
+// chain to the handler installed before us (Python's faulthandler prints the Python stacks, then the
+// default action dumps core).  An abort raised inside a C++ destructor during garbage collection --
+// an error from an earlier asynchronous GPU failure surfacing in a free -- otherwise shows only
+// "Fatal Python error: Aborted ... Garbage-collecting" (profiles/r4_decode_attn_trace_abort.txt).
+// NXD_ABORT_BACKTRACE=0 leaves SIGABRT alone.
+static struct sigaction g_prev_abrt;
+static void abort_backtrace(int sig) {
+  static const char hdr[] = "[nxd] SIGABRT: native backtrace (neuronx_distributed_llama3_2_amd _C)\n";
+  (void)!write(2, hdr, sizeof(hdr) - 1);
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, n, 2);
+  sigaction(SIGABRT, &g_prev_abrt, nullptr);
+  raise(sig);
+}
+static void install_abort_backtrace() {
+  const char* e = std::getenv("NXD_ABORT_BACKTRACE");
+  if (e && e[0] == '0') return;
+  struct sigaction sa {};
+  sa.sa_handler = abort_backtrace;
+  sigemptyset(&sa.sa_mask);
+  sa.sa_flags = SA_RESETHAND;
+  sigaction(SIGABRT, &sa, &g_prev_abrt);
+}
+
 PYBIND11_MODULE(_C, m) {
+  install_abort_backtrace();
+  m.def("decode_attn_trace", [](c10::optional<at::Tensor> t) {
+    if (!t.has_value()) {
+      nxd::decode_attn_set_trace(nullptr);
+      return;
+    }
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->is_contiguous(), "trace: int64 GPU tensor");
+    nxd::decode_attn_set_trace(reinterpret_cast<uint64_t*>(t->data_ptr<int64_t>()));
+  }, "arm (tensor) / disarm (None) the decode attention phase trace");
   register_gemm(m);
   register_dataloader(m);
   register_comm(m);

@@ -25,6 +25,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace nxd {
 namespace dattn {
@@ -58,7 +59,16 @@ struct Params {
   int64_t ldwo;
   float* oacc;
   int Hout, R, NP;     // output rows, row chunks per kv head, Wo register passes (<= 4)
+  // opt-in phase trace (decode_attn_set_trace): wave 0 of each workgroup stores s_memrealtime (100 MHz)
+  // at entry and exit to trace[2 * blockIdx.x + {0, 1}]; null = off.  This is the trailing field whose
+  // round-4 version aborted the decode tests: decode_attn2_launch built `Params p;` without value-
+  // initialisation, so the field was stack garbage (non-null) there and the kernel stored through it
+  // (profiles/r4_decode_attn_trace_abort.txt).  Every launcher now value-initialises its Params.
+  uint64_t* trace;
 };
+static_assert(std::is_trivially_copyable<Params>::value && sizeof(Params) <= 4096, "kernel-argument struct");
+
+static uint64_t* g_trace = nullptr;
 
 // Prefetch workgroup body: 4 independent 16-B loads in flight per lane, folded into one value that
 // is stored only under a condition the host never creates (pf_n16[0] < 0), so the loads stay live.
@@ -99,6 +109,7 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
     prefetch_body(p, blockIdx.x - p.attn_wgs, gridDim.x - p.attn_wgs);
     return;
   }
+  if (p.trace != nullptr && tid == 0) p.trace[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   const int split = FUSE ? 0 : (int)blockIdx.x % p.nsplit;
   const int bh = FUSE ? (int)blockIdx.x / p.R : (int)blockIdx.x / p.nsplit;
   const int b = bh / p.Hkv, hkv = bh % p.Hkv;
@@ -319,6 +330,7 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
       }
     }
   }
+  if (p.trace != nullptr && tid == 0) p.trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Pending prefetch of the next decode_attn2 launch (set by decode_attn_set_prefetch, consumed by
@@ -329,6 +341,10 @@ static int64_t g_pf_bytes[2] = {0, 0};
 static int g_pf_wgs = 0;
 
 }  // namespace dattn
+
+// Opt-in phase trace of the following decode attention launches (eager or captured: the pointer is
+// recorded by value); null turns it off.  trace must hold 2 x (launch grid) uint64.
+void decode_attn_set_trace(uint64_t* trace) { dattn::g_trace = trace; }
 
 void decode_attn_set_prefetch(const void* a, int64_t a_bytes, const void* b, int64_t b_bytes, int wgs) {
   dattn::g_pf[0] = a; dattn::g_pf_bytes[0] = a ? a_bytes : 0;
@@ -344,7 +360,7 @@ int decode_attn2_launch(const void* q, const int64_t* qs, const void* kc, const 
   if (Hkv <= 0 || Hq % Hkv) return -1;
   const int M = (Hq / Hkv) * T;
   if (M > 16 || (D != 64 && D != 128)) return -1;
-  dattn::Params p;
+  dattn::Params p{};   // value-initialised: every field a launcher does not set is zero / null
   p.q = (const uint16_t*)q; p.q_sb = qs[0]; p.q_st = qs[1]; p.q_sh = qs[2];
   p.kc = (const uint16_t*)kc; p.vc = (const uint16_t*)vc;
   p.c_sb = cs[0]; p.c_sh = cs[1]; p.c_sl = cs[2];
@@ -359,6 +375,7 @@ int decode_attn2_launch(const void* q, const int64_t* qs, const void* kc, const 
   const int nwv = D == 64 ? 8 : 4;
   const size_t lds = (size_t)nwv * dattn::KB * D * 2 + (size_t)nwv * 16 * D * 4 + (size_t)2 * nwv * 16 * 4;
   p.attn_wgs = B * Hkv * p.nsplit;
+  p.trace = dattn::g_trace;
   int pf_wgs = 0;
   for (int r = 0; r < 2; ++r) {
     // 16-B aligned start, whole chunks only (a prefetch never needs the ragged tail)
@@ -414,6 +431,7 @@ int decode_attn_oproj_launch(const void* q, const int64_t* qs, const void* kc, c
   p.scale_log2 = scale * 1.4426950408889634f;
   p.wo = (const uint16_t*)wo; p.ldwo = ldwo; p.oacc = oacc; p.Hout = Hout; p.R = R; p.NP = Hout / R / rpp;
   p.attn_wgs = B * Hkv * R;
+  p.trace = dattn::g_trace;
   const size_t lds = (size_t)nwv * dattn::KB * D * 2 + (size_t)nwv * 16 * D * 4 + (size_t)2 * nwv * 16 * 4;
   const dim3 grid(p.attn_wgs), block(nt);
   static const bool wo_late = [] {

@@ -962,7 +962,7 @@ int flash_attn_bwd_launch(const void* q, const void* k, const void* v, const voi
                          dq_zero, (int)Sq_pad);
   }
 
-  BwdParams p;
+  BwdParams p{};
   p.q = (const uint16_t*)q; p.k = (const uint16_t*)k; p.v = (const uint16_t*)v; p.dout = (const uint16_t*)dout;
   p.nlse = nlse; p.ndelta = ndelta; p.dq_acc = dq_acc; p.dk_acc = dk_acc; p.dv_acc = dv_acc;
   p.dk_slab = dk_slab; p.dv_slab = dv_slab;

@@ -354,7 +354,7 @@ int flash_attn_fwd_launch(const void* q, const void* k, const void* v, void* o, 
                           int B, int Sq, int Sk, int Hq, int Hkv, int D, float softmax_scale,
                           int causal, int causal_offset, const DropoutArgs& drop, hipStream_t stream) {
   using namespace fa;
-  FwdParams p;
+  FwdParams p{};
   p.q = (const uint16_t*)q;
   p.k = (const uint16_t*)k;
   p.v = (const uint16_t*)v;

@@ -553,7 +553,7 @@ int decode_attn_launch(const void* q, const int64_t* qs, const void* kc, const v
     }
     if (rc != -1) return rc;   // -1: shape not covered by the MFMA kernel
   }
-  DecodeParams p;
+  DecodeParams p{};
   p.q = (const uint16_t*)q; p.q_sb = qs[0]; p.q_st = qs[1]; p.q_sh = qs[2];
   p.kc = (const uint16_t*)kc; p.vc = (const uint16_t*)vc;
   p.c_sb = cs[0]; p.c_sh = cs[1]; p.c_sl = cs[2];

@@ -408,3 +408,40 @@ def test_greedy_fused_decode_matches_unfused(hf_sd):
         finally:
             graphs.GREEDY_FUSED = True
     assert torch.equal(outs[0], outs[1])
+
+
+def test_decode_attention_phase_trace(monkeypatch):
+    """The opt-in phase trace of the decode attention launches (decode_attn.hip Params::trace, the
+    trailing field whose round-4 version aborted these tests while one launcher left it
+    uninitialised): armed, each workgroup stamps entry <= exit; disarmed, decode output is unchanged."""
+    from transformers import LlamaConfig, LlamaForCausalLM as HF
+    from neuronx_distributed_llama3_2_amd.inference import model_base
+    from neuronx_distributed_llama3_2_amd import _C
+
+    cfg = LlamaConfig(hidden_size=512, intermediate_size=1024, num_hidden_layers=2, num_attention_heads=8,
+                      num_key_value_heads=2, vocab_size=1000, max_position_embeddings=1024, rms_norm_eps=1e-5,
+                      rope_theta=500000.0, tie_word_embeddings=False, eos_token_id=2)
+    torch.manual_seed(0)
+    sd = {k: v.detach().clone() for k, v in HF(cfg).state_dict().items()}
+    m = _model(cfg, sd, torch.bfloat16, graphs=False, steps=1, device=torch.device("cuda"))
+    ids = torch.randint(3, cfg.vocab_size, (1, 21))
+    m.generate(ids, max_new_tokens=2, eos_token_id=-1)
+    last = torch.randint(3, cfg.vocab_size, (1, 1)).cuda()
+    pos = torch.full((1, 1), 23, dtype=torch.int64, device="cuda")
+    sid = torch.arange(1, device="cuda")
+    clen = torch.full((1,), 24, dtype=torch.int32, device="cuda")
+    for fused in (True, False):
+        monkeypatch.setattr(model_base, "_ATTN_OPROJ", fused)
+        ref = m.model.forward_tokens(last, pos, sid, clen).float()
+        tr = torch.zeros(2 * 4096, dtype=torch.int64, device="cuda")
+        _C.decode_attn_trace(tr)
+        try:
+            out = m.model.forward_tokens(last, pos, sid, clen).float()
+        finally:
+            _C.decode_attn_trace(None)
+        torch.cuda.synchronize()
+        t = tr.view(-1, 2).cpu()
+        hit = t[:, 0] > 0
+        assert hit.any() and bool((t[hit, 1] >= t[hit, 0]).all()), t[:8]
+        if not fused:
+            assert torch.equal(out, ref)
