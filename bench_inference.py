@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--runs", type=int, default=10)
     ap.add_argument("--graph-steps", type=int, default=16)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--gloo-gpu", action="store_true",
+                    help="TP rehearsal on a one-GPU box: every rank on cuda:0, gloo process group (the decode "
+                         "all-reduces still run the one-shot peer kernel over IPC); eager decode")
     ap.add_argument("--quantized", default=None, choices=[None, "per_tensor_symmetric", "per_channel_symmetric"])
     ap.add_argument("--report", default="gpurun_out/benchmark_report.json")
     ap.add_argument("--weight-layout", action="store_true",
@@ -36,10 +39,14 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.gloo_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.gloo_gpu:
+            dist.init_process_group("gloo")
+            args.no_graphs = True   # gloo collectives (vocab gather) are host-staged: not capturable
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from neuronx_distributed_llama3_2_amd.inference import InferenceConfig, LlamaForCausalLMInference
     from neuronx_distributed_llama3_2_amd.inference.benchmark import Benchmark, generate_report
     from neuronx_distributed_llama3_2_amd.models.llama.modeling_llama import llama_config
@@ -77,7 +84,7 @@ def main():
     cte_ms = report["context_encoding_model"]["latency_ms_p50"]
     report["token_generation"] = {"ms_per_token_p50": (e2e_ms - cte_ms) / max(1, args.new - 1),
                                   "tokens_per_s_per_seq": 1000.0 * max(1, args.new - 1) / max(1e-6, e2e_ms - cte_ms)}
-    report["config"] = {"model": args.model, "tp": world, "batch": args.batch, "prompt": args.prompt,
+    report["config"] = {"model": args.model, "tp": world, "gloo_gpu_rehearsal": bool(args.gloo_gpu), "batch": args.batch, "prompt": args.prompt,
                         "new_tokens": args.new, "dtype": "bf16", "graph_steps": args.graph_steps,
                         "hip_graphs": not args.no_graphs, "quantized": args.quantized,
                         "weight_layouts": None if layouts is None else {v: sum(1 for x in layouts.values() if x == v)

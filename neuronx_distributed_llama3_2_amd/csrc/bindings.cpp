@@ -65,7 +65,7 @@ void decode_attn_set_prefetch(const void*, int64_t, const void*, int64_t, int);
 void decode_attn_set_trace(uint64_t*);
 int dgemv_launch(int, const void*, int64_t, const void*, float, const void*, int64_t, void*, int64_t, int, int, int, int,
                  int, int, const float*, const float*, const int64_t*, int, void*, void*, int64_t, int64_t, int64_t,
-                 const int*, int, int, const float*, float*, hipStream_t, const int64_t*, int64_t, void*);
+                 const int*, int, int, const float*, float*, hipStream_t, const int64_t*, int64_t, void*, float*);
 int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, int, hipStream_t);
 int wgrad_gemm_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int, int, int, int, hipStream_t);
 int wgrad_gemm_choose_splits(int, int, int);
@@ -866,7 +866,14 @@ void dgemv(int64_t epi, at::Tensor x, c10::optional<at::Tensor> norm_w, double e
            c10::optional<at::Tensor> xidx, c10::optional<at::Tensor> xcopy) {
   check_bf16(x, "x");
   check_bf16(w, "w");
-  check_bf16(y, "y");
+  // epi 0 with an fp32 y: the unrounded partial sum (row-parallel projection at TP > 1)
+  float* yf = nullptr;
+  if (epi == 0 && y.scalar_type() == at::kFloat) {
+    TORCH_CHECK(y.is_cuda(), "dgemv: y must be a GPU tensor");
+    yf = y.data_ptr<float>();
+  } else {
+    check_bf16(y, "y");
+  }
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "dgemv: x [M, K], w [Nw, K], y [M, N]");
   TORCH_CHECK(x.stride(1) == 1 && w.stride(1) == 1 && y.stride(1) == 1, "dgemv: unit inner strides");
   // xidx (QKV only): x is an embedding table [V, K] and input row m is x[xidx[m]]; xcopy [M, K]
@@ -959,7 +966,7 @@ void dgemv(int64_t epi, at::Tensor x, c10::optional<at::Tensor> norm_w, double e
   }
   check_rc(nxd::dgemv_launch((int)epi, x.data_ptr(), x.stride(0), nw, (float)eps, w.data_ptr(), w.stride(0), y.data_ptr(),
                              y.stride(0), (int)M, (int)N, (int)K, (int)nq, (int)nkv, (int)D, cp, sp, pp, (int)T, kp, vp,
-                             c_sb, c_sh, c_sl, ci, Lmax, max_pos, xa, ya, cur_stream(), xi, x.size(0), xc),
+                             c_sb, c_sh, c_sl, ci, Lmax, max_pos, xa, ya, cur_stream(), xi, x.size(0), xc, yf),
            "dgemv");
 }
 

@@ -13,6 +13,7 @@
 #include <torch/extension.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <ATen/hip/HIPContext.h>
 
 #include <dlfcn.h>
 
@@ -24,6 +25,13 @@
 
 namespace nxd {
 int multi_copy_launch(const void* const*, void* const*, const int64_t*, int, hipStream_t);
+// peer_allreduce.hip: one-shot all-reduce over IPC-mapped peer buffers
+void* peer_ar_create(int, int*);
+int peer_ar_ipc_handle(void*, void*);
+int peer_ar_open(void*, int, int, const void*);
+int peer_ar_run(void*, float*, int, int, int, float*, void*, const float*, hipStream_t);
+int peer_ar_error(void*);
+void peer_ar_destroy(void*);
 }
 
 namespace {
@@ -289,6 +297,59 @@ int64_t bucketed_all_reduce(int64_t h, std::vector<at::Tensor> ts, at::Tensor st
   return off;
 }
 
+// ---- one-shot peer all-reduce (csrc/peer_allreduce.hip) ---------------------------------------------
+// Latency-class all-reduce of tensor-parallel decode partials: every rank exports one device region
+// (IPC handle exchanged by the caller over the torch process group), maps every peer's, and one kernel
+// per call publishes, waits for and sums all partials.  Modes: 0 out = sum, 1 residual fold
+// res = bf16(bf16(res + bf16(xadd)) + bf16(sum)), 2 res = bf16(sum).
+pybind11::tuple peer_ar_create(int64_t nmax) {
+  int unc = 0;
+  void* h = nxd::peer_ar_create((int)nmax, &unc);
+  TORCH_CHECK(h, "peer all-reduce: device allocation failed");
+  return pybind11::make_tuple(reinterpret_cast<int64_t>(h), unc != 0);
+}
+
+pybind11::bytes peer_ar_ipc_handle(int64_t h) {
+  char buf[64] = {0};
+  const int n = nxd::peer_ar_ipc_handle(reinterpret_cast<void*>(h), buf);
+  TORCH_CHECK(n > 0, "peer all-reduce: hipIpcGetMemHandle failed");
+  return pybind11::bytes(buf, 64);
+}
+
+void peer_ar_open(int64_t h, int64_t rank, std::vector<std::string> handles) {
+  std::string all;
+  for (auto& x : handles) {
+    TORCH_CHECK(x.size() == 64, "peer all-reduce: 64-byte IPC handles expected");
+    all += x;
+  }
+  const int rc = nxd::peer_ar_open(reinterpret_cast<void*>(h), (int)handles.size(), (int)rank, all.data());
+  TORCH_CHECK(rc == 0, "peer all-reduce: opening the peers' IPC handles failed (", rc, ")");
+}
+
+void peer_ar_run(int64_t h, at::Tensor in, bool zero_in, int64_t mode, c10::optional<at::Tensor> out,
+                 c10::optional<at::Tensor> res, c10::optional<at::Tensor> xadd) {
+  TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kFloat && in.is_contiguous(), "peer all-reduce: fp32 input");
+  const int64_t n = in.numel();
+  float* op = nullptr;
+  void* rp = nullptr;
+  const float* xp = nullptr;
+  if (out.has_value()) {
+    TORCH_CHECK(out->scalar_type() == at::kFloat && out->is_contiguous() && out->numel() == n, "peer all-reduce: out");
+    op = out->data_ptr<float>();
+  }
+  if (res.has_value()) {
+    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->is_contiguous() && res->numel() == n, "peer all-reduce: res");
+    rp = res->data_ptr();
+  }
+  if (xadd.has_value()) {
+    TORCH_CHECK(xadd->scalar_type() == at::kFloat && xadd->is_contiguous() && xadd->numel() >= n, "peer all-reduce: xadd");
+    xp = xadd->data_ptr<float>();
+  }
+  const int rc = nxd::peer_ar_run(reinterpret_cast<void*>(h), in.data_ptr<float>(), zero_in ? 1 : 0, (int)mode, (int)n, op,
+                                  rp, xp, at::hip::getCurrentHIPStream().stream());
+  TORCH_CHECK(rc == 0, "peer all-reduce: launch failed (", rc, ")");
+}
+
 std::string version() {
   int v = 0;
   need_rccl();
@@ -310,4 +371,12 @@ void register_comm(pybind11::module& m) {
   m.def("comm_batch_p2p", &batch_p2p);
   m.def("comm_bucketed_all_reduce", &bucketed_all_reduce);
   m.def("comm_version", &version);
+  m.def("peer_ar_create", &peer_ar_create);
+  m.def("peer_ar_ipc_handle", &peer_ar_ipc_handle);
+  m.def("peer_ar_open", &peer_ar_open);
+  m.def("peer_ar_run", &peer_ar_run, pybind11::arg("h"), pybind11::arg("inp"), pybind11::arg("zero_in"),
+        pybind11::arg("mode"), pybind11::arg("out") = pybind11::none(), pybind11::arg("res") = pybind11::none(),
+        pybind11::arg("xadd") = pybind11::none());
+  m.def("peer_ar_error", [](int64_t h) { return nxd::peer_ar_error(reinterpret_cast<void*>(h)); });
+  m.def("peer_ar_destroy", [](int64_t h) { nxd::peer_ar_destroy(reinterpret_cast<void*>(h)); });
 }

@@ -63,6 +63,9 @@ struct Params {
   const int64_t* xidx;
   int64_t xrows;
   uint16_t* xcopy;
+  // PLAIN only: fp32 output [M, N] (row stride ldy) instead of bf16 y -- a row-parallel projection's
+  // partial sum kept unrounded for the tensor-parallel all-reduce (decode at TP > 1)
+  float* yf;
 };
 
 constexpr int U = 4;   // 512-element k-steps per load round
@@ -399,6 +402,7 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
           }
           yr[n] = f2bf(yv + bf2f(f2bf(acc[m][r])));
         }
+        else if (EPI == PLAIN && p.yf) p.yf[(int64_t)m * p.ldy + n] = acc[m][r];
         else yr[n] = f2bf(acc[m][r]);
       }
     }
@@ -517,7 +521,8 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
                  int64_t ldy, int M, int N, int K, int nq, int nkv, int D, const float* cos_t, const float* sin_t,
                  const int64_t* pos, int T, void* kc, void* vc, int64_t c_sb, int64_t c_sh, int64_t c_sl,
                  const int* cache_idx, int Lmax, int max_pos, const float* xadd, float* yadd, hipStream_t stream,
-                 const int64_t* xidx, int64_t xrows, void* xcopy) {
+                 const int64_t* xidx, int64_t xrows, void* xcopy, float* yf) {
+  if (yf && epi != dfused::PLAIN) return -5;
   if (M < 1 || M > 8 || N < 1 || K < 8 || (K % 8)) return -1;
   if ((xadd && !norm_w) || (yadd && epi != dfused::RESID)) return -3;
   if (xidx && (epi != dfused::ROPE_KV || !norm_w || xrows < 1)) return -4;
@@ -534,6 +539,7 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
   p.xidx = xidx;
   p.xrows = xrows;
   p.xcopy = static_cast<uint16_t*>(xcopy);
+  p.yf = yf;
   if (dfused::g_occ < 0) {
     const char* e = getenv("NXD_DECODE_OCC");
     dfused::g_occ = e ? atoi(e) : 0;

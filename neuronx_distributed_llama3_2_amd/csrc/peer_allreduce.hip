@@ -1,0 +1,271 @@
+// One-shot all-reduce over peer-mapped (IPC) device buffers for latency-bound messages: the
+// tensor-parallel decode's row-parallel partial sums (o_proj, down: M x H fp32, a few KiB per layer).
+//
+// Reference: the fork's TP decode has its all-reduces compiled into one SPMD graph
+// (examples/inference/modules/gqa.py:641-647, src/neuronx_distributed/trace/spmd.py:82-187).  A ring
+// all-reduce through RCCL costs (2 (W - 1)) link latencies per call; at these sizes the data is
+// nothing and the latency is everything, so here every rank publishes its partial once and every rank
+// reads all W partials directly: ONE kernel launch per all-reduce, no host involvement, capturable in
+// the decode hipGraph.
+//
+// Per rank, one IPC-exported region: flags [2][kMaxBlocks] (uint64 epochs) + slots [2][nmax] fp32.
+// Call c of a rank has epoch e = ctr[b] + 1 (per-block device counter, so hipGraph replays keep
+// counting) and parity e & 1.  Block b of every rank:
+//   1. copies its chunk of the local partial into slot[parity] (and zeroes the partial when it is an
+//      atomic accumulator that must start at zero for the next producer);
+//   2. publishes: every wave drains its stores (vmcnt(0)), workgroup barrier, one system-scope release
+//      (the region may be read from another GPU over xGMI), then the flag[parity][b] = e store;
+//   3. waits for flag[parity][b] >= e of every peer (relaxed system-scope polls with s_sleep and a
+//      bounded spin -- an absent peer sets *err and the kernel still exits), then one system-scope
+//      acquire and a barrier;
+//   4. sums the W chunks in rank order (bitwise identical on every rank: the residual stream stays
+//      replicated) and applies the epilogue.
+// A slot is rewritten two calls later; by then every peer has passed the intervening call, which it
+// only enters after finishing its reads of this one, so two slots suffice.
+#include "common.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+namespace nxd {
+namespace par {
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 64;
+constexpr int kThreads = 256;
+
+enum Mode { SUM = 0, FOLD_RES = 1, SET_RES = 2 };
+
+struct Args {
+  float* in;                                 // local partial [n] fp32
+  int zero_in;                               // zero `in` after publishing it
+  float* slot[2];                            // this rank's slots (IPC region)
+  const float* peer_slot[kMaxRanks][2];      // every rank's slots (own included), as mapped here
+  uint64_t* flag;                            // this rank's flags [2][kMaxBlocks] (IPC region)
+  const uint64_t* peer_flag[kMaxRanks];      // every rank's flags, as mapped here
+  uint64_t* ctr;                             // [kMaxBlocks] epochs (local memory)
+  int* err;                                  // > 0: a peer never arrived (bounded spin expired)
+  int world, rank, n, chunk, mode;
+  int64_t spin_limit;
+  float* out;                                // SUM: [n] fp32
+  uint16_t* res;                             // FOLD_RES / SET_RES: bf16 residual stream [n]
+  const float* xadd;                         // FOLD_RES: pending fp32 sum folded first (o_proj)
+};
+
+__global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
+  __shared__ uint64_t e_s;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int lo = b * a.chunk, hi = min(a.n, lo + a.chunk);
+  if (tid == 0) e_s = a.ctr[b] + 1;
+  __syncthreads();
+  const uint64_t e = e_s;
+  const int par = (int)(e & 1);
+  float* mine = a.slot[par];
+  for (int i = lo + tid * 4; i < hi; i += kThreads * 4) {
+    if (i + 4 <= hi) {
+      const f32x4_t v = *reinterpret_cast<const f32x4_t*>(a.in + i);
+      *reinterpret_cast<f32x4_t*>(mine + i) = v;
+      if (a.zero_in) *reinterpret_cast<f32x4_t*>(a.in + i) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    } else {
+      for (int j = i; j < hi; ++j) {
+        mine[j] = a.in[j];
+        if (a.zero_in) a.in[j] = 0.f;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: peers may sit on other GPUs
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(a.flag + par * kMaxBlocks + b, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // (rank loops unrolled with static indices: a runtime index into the kernel-argument arrays would
+  // copy them to scratch)
+  const uint64_t* pf = nullptr;
+#pragma unroll
+  for (int r = 0; r < kMaxRanks; ++r)
+    if (r == tid) pf = a.peer_flag[r] + par * kMaxBlocks + b;
+  if (tid < a.world && tid != a.rank) {
+    int64_t it = 0;
+    while (__hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > a.spin_limit) {
+        atomicAdd(a.err, 1);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int i = lo + tid; i < hi; i += kThreads) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r)
+      if (r < a.world) s += (par ? a.peer_slot[r][1] : a.peer_slot[r][0])[i];
+    if (a.mode == SUM) {
+      a.out[i] = s;
+    } else if (a.mode == FOLD_RES) {
+      // the unfused TP = 1 rounding: y = bf16(bf16(y + bf16(o_proj)) + bf16(down))
+      const float y = bf2f(f2bf(bf2f(a.res[i]) + bf2f(f2bf(a.xadd[i]))));
+      a.res[i] = f2bf(y + bf2f(f2bf(s)));
+    } else {
+      a.res[i] = f2bf(s);
+    }
+  }
+  if (tid == 0) a.ctr[b] = e;
+}
+
+struct Handle {
+  char* base = nullptr;        // IPC region: flags, slot 0, slot 1
+  size_t bytes = 0;
+  int nmax = 0;
+  bool uncached = false;
+  int world = 0, rank = 0;
+  char* peer_base[kMaxRanks] = {};
+  bool opened[kMaxRanks] = {};
+  uint64_t* ctr = nullptr;
+  int* err = nullptr;
+};
+
+constexpr size_t kFlagBytes = 2 * kMaxBlocks * sizeof(uint64_t);
+
+size_t slot_offset(int nmax, int s) {
+  const size_t slot_bytes = ((size_t)nmax * 4 + 255) / 256 * 256;
+  return 1024 + (size_t)s * slot_bytes;
+}
+
+}  // namespace par
+
+// ---- host API (comm.cpp binds it) ----------------------------------------------------------------
+
+void* peer_ar_create(int nmax, int* uncached) {
+  auto* h = new par::Handle();
+  h->nmax = nmax;
+  h->bytes = par::slot_offset(nmax, 2);
+  static_assert(par::kFlagBytes <= 1024, "flag block");
+  // fine-grained, uncached device memory: coherent for peers on other GPUs without relying on cache
+  // maintenance; plain device memory if the runtime cannot export such an allocation
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, h->bytes, hipDeviceMallocUncached) == hipSuccess) {
+    hipIpcMemHandle_t ih;
+    if (hipIpcGetMemHandle(&ih, p) == hipSuccess) {
+      h->uncached = true;
+    } else {
+      (void)hipGetLastError();
+      (void)hipFree(p);
+      p = nullptr;
+    }
+  } else {
+    (void)hipGetLastError();
+    p = nullptr;
+  }
+  if (!p && hipMalloc(&p, h->bytes) != hipSuccess) {
+    delete h;
+    return nullptr;
+  }
+  h->base = static_cast<char*>(p);
+  if (hipMemset(h->base, 0, h->bytes) != hipSuccess || hipMalloc(&h->ctr, par::kMaxBlocks * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(h->ctr, 0, par::kMaxBlocks * sizeof(uint64_t)) != hipSuccess || hipMalloc(&h->err, sizeof(int)) != hipSuccess ||
+      hipMemset(h->err, 0, sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    delete h;
+    return nullptr;
+  }
+  *uncached = h->uncached ? 1 : 0;
+  return h;
+}
+
+int peer_ar_ipc_handle(void* hv, void* out64) {
+  auto* h = static_cast<par::Handle*>(hv);
+  hipIpcMemHandle_t ih;
+  if (hipIpcGetMemHandle(&ih, h->base) != hipSuccess) return -1;
+  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "ipc handle size");
+  memcpy(out64, &ih, sizeof(ih));
+  return (int)sizeof(ih);
+}
+
+// handles: world x 64 bytes (every rank's region, own included)
+int peer_ar_open(void* hv, int world, int rank, const void* handles) {
+  auto* h = static_cast<par::Handle*>(hv);
+  if (world < 1 || world > par::kMaxRanks || rank < 0 || rank >= world) return -1;
+  h->world = world;
+  h->rank = rank;
+  for (int r = 0; r < world; ++r) {
+    if (r == rank) {
+      h->peer_base[r] = h->base;
+      continue;
+    }
+    hipIpcMemHandle_t ih;
+    memcpy(&ih, static_cast<const char*>(handles) + 64 * r, sizeof(ih));
+    void* p = nullptr;
+    if (hipIpcOpenMemHandle(&p, ih, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -2 - r;
+    h->peer_base[r] = static_cast<char*>(p);
+    h->opened[r] = true;
+  }
+  return 0;
+}
+
+int peer_ar_run(void* hv, float* in, int zero_in, int mode, int n, float* out, void* res, const float* xadd,
+                hipStream_t stream) {
+  auto* h = static_cast<par::Handle*>(hv);
+  if (n < 1 || n > h->nmax || h->world < 1) return -1;
+  if ((mode == par::SUM && !out) || (mode != par::SUM && !res) || (mode == par::FOLD_RES && !xadd)) return -2;
+  if ((reinterpret_cast<uintptr_t>(in) & 15) || n % 4) return -3;
+  par::Args a{};
+  a.in = in;
+  a.zero_in = zero_in;
+  for (int s = 0; s < 2; ++s) a.slot[s] = reinterpret_cast<float*>(h->base + par::slot_offset(h->nmax, s));
+  for (int r = 0; r < h->world; ++r) {
+    for (int s = 0; s < 2; ++s) a.peer_slot[r][s] = reinterpret_cast<const float*>(h->peer_base[r] + par::slot_offset(h->nmax, s));
+    a.peer_flag[r] = reinterpret_cast<const uint64_t*>(h->peer_base[r]);
+  }
+  a.flag = reinterpret_cast<uint64_t*>(h->base);
+  a.ctr = h->ctr;
+  a.err = h->err;
+  a.world = h->world;
+  a.rank = h->rank;
+  a.n = n;
+  a.mode = mode;
+  // ~1 KiB of fp32 per block keeps every CU's share latency-sized; at most kMaxBlocks blocks
+  int blocks = (n + 1023) / 1024;
+  blocks = blocks < 1 ? 1 : (blocks > par::kMaxBlocks ? par::kMaxBlocks : blocks);
+  a.chunk = ((n + blocks - 1) / blocks + 3) / 4 * 4;
+  blocks = (n + a.chunk - 1) / a.chunk;
+  static const int64_t limit = [] {
+    const char* e = getenv("NXD_PEER_AR_SPIN_LIMIT");
+    return e ? atoll(e) : (int64_t)1 << 24;   // ~ seconds of s_sleep polling, then give up
+  }();
+  a.spin_limit = limit;
+  a.out = out;
+  a.res = static_cast<uint16_t*>(res);
+  a.xadd = xadd;
+  hipLaunchKernelGGL(par::peer_allreduce_kernel, dim3(blocks), dim3(par::kThreads), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+int peer_ar_error(void* hv) {
+  auto* h = static_cast<par::Handle*>(hv);
+  int v = 0;
+  if (hipMemcpy(&v, h->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return v;
+}
+
+void peer_ar_destroy(void* hv) {
+  auto* h = static_cast<par::Handle*>(hv);
+  if (!h) return;
+  (void)hipDeviceSynchronize();
+  for (int r = 0; r < par::kMaxRanks; ++r)
+    if (h->opened[r]) (void)hipIpcCloseMemHandle(h->peer_base[r]);
+  if (h->base) (void)hipFree(h->base);
+  if (h->ctr) (void)hipFree(h->ctr);
+  if (h->err) (void)hipFree(h->err);
+  delete h;
+}
+
+}  // namespace nxd

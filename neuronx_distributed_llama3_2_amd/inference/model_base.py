@@ -158,7 +158,9 @@ class DecoderInferenceMixin:
         return ok and input_ids.is_cuda and M <= 8 and M * self.config.hidden_size <= 32768
 
     def _check_decode_fusable(self) -> bool:
-        if os.environ.get("NXD_DECODE_FUSED", "1") == "0" or self.tp != 1:
+        if os.environ.get("NXD_DECODE_FUSED", "1") == "0":
+            return False
+        if self.tp > 1 and os.environ.get("NXD_DECODE_FUSED_TP", "1") == "0":
             return False
         if type(self)._qkv_hook is not DecoderInferenceMixin._qkv_hook or type(self)._norm is not DecoderInferenceMixin._norm:
             return False
@@ -184,6 +186,8 @@ class DecoderInferenceMixin:
         return buf
 
     def _forward_decode_fused(self, input_ids, positions, seq_ids, cache_len, last_index, return_hidden):
+        if self.tp > 1:
+            return self._forward_decode_fused_tp(input_ids, positions, seq_ids, cache_len, last_index, return_hidden)
         C = ops.ext()
         B, T = input_ids.shape
         M = B * T
@@ -244,6 +248,80 @@ class DecoderInferenceMixin:
         C.dgemv(0, h2, self.model.norm.weight, self.eps, self.lm_head.weight, logits, 0, 0, 0, None, None, None, 1,
                 None, None, None)                                       # final norm + lm_head
         logits = logits.view(h.shape[:-1] + (logits.shape[-1],))
+        if return_hidden:
+            return logits, ops.rms_norm(h, self.model.norm.weight, self.eps)[0]
+        return logits
+
+    def _decode_tp_state(self, H: int, device):
+        """TP > 1 fused decode: fp32 [8, H] partial / sum buffers and the decode all-reduce (one-shot
+        peer all-reduce over IPC when available -- parallel/peer_allreduce.py -- else the process
+        group).  Built once; its collective set-up runs on every rank at the same decode step."""
+        st = getattr(self, "_tp_dec", None)
+        if st is None or st["H"] != H or st["device"] != device:
+            from ..parallel.peer_allreduce import make_decode_all_reduce
+
+            ar = make_decode_all_reduce(ps.get_tensor_model_parallel_group(), 8 * H, device,
+                                        prefer_peer=os.environ.get("NXD_DECODE_PEER_AR", "1") == "1")
+            z = lambda: torch.zeros((8, H), dtype=torch.float32, device=device)  # noqa: E731
+            st = self._tp_dec = {"H": H, "device": device, "ar": ar, "oacc": z(), "osum": z(), "dacc": z(), "emb": z()}
+        return st
+
+    def _forward_decode_fused_tp(self, input_ids, positions, seq_ids, cache_len, last_index, return_hidden):
+        """Decode at TP > 1 on the fused GEMV kernels.  Per layer (6 launches):
+          RMSNorm+QKV+RoPE+KV-write on this rank's heads; attention + o_proj partial (fp32 atomics
+          into oacc); all-reduce oacc -> osum; RMSNorm(res + osum)+gate_up+SwiGLU on this rank's
+          intermediate slice; down partial (fp32); all-reduce it and fold res = bf16(bf16(res +
+          bf16(osum)) + bf16(down)) -- the TP = 1 kernels' rounding, with the partials summed in fp32
+          in rank order (identical bits on every rank).  The embedding is the vocab-parallel gather
+          summed the same way; lm_head runs on this rank's vocabulary slice, gathered at the end.
+        Reference: examples/inference/modules/gqa.py:641-647 (the TP all-reduces of the fork's
+        notebook config, tp_degree = 2), src/neuronx_distributed/trace/spmd.py:82-187."""
+        C = ops.ext()
+        B, T = input_ids.shape
+        M = B * T
+        nq, nkv, D = self.nq, self.nkv, self.head_dim
+        W = (nq + 2 * nkv) * D
+        cos_t, sin_t = self.model.rope_cache.tables(input_ids.device)
+        pos = positions.reshape(-1).to(torch.int64).contiguous()
+        sid32 = seq_ids.to(torch.int32).contiguous() if seq_ids is not None else None
+        emb = self.model.embed_tokens
+        ew = emb.weight
+        H = ew.shape[1]
+        st = self._decode_tp_state(H, ew.device)
+        ar, oacc, osum, dacc = st["ar"], st["oacc"], st["osum"], st["dacc"]
+        res = torch.empty((M, H), dtype=ew.dtype, device=ew.device)
+        ebuf = st["emb"][:M]
+        ebuf.copy_(ops.vocab_parallel_embedding(input_ids, ew, emb.start_index).reshape(M, H))
+        ar.set_residual_(ebuf, res)                                   # res = the embedding rows
+        qkv = torch.empty((M, W), dtype=res.dtype, device=res.device)
+        clen32 = cache_len.to(torch.int32)
+        fuse_o = _ATTN_OPROJ and not getattr(self, "_decode_deterministic", False)
+        for i, layer in enumerate(self.model.layers):
+            attn = layer.self_attn
+            w_qkv = attn.qkv_proj._fused_weight_bias()[0] if hasattr(attn.qkv_proj, "_fused_weight_bias") \
+                else attn.qkv_proj.weight
+            kc, vc = self.kv_cache[i, 0], self.kv_cache[i, 1]
+            C.dgemv(3, res, layer.input_layernorm.weight, self.eps, w_qkv, qkv, nq, nkv, D, cos_t, sin_t, pos, T,
+                    kc, vc, sid32)
+            q = qkv.view(B, T, nq + 2 * nkv, D)[:, :, :nq]
+            ln2, w_gu, w_d = self._fused_ffn_weights(layer)
+            if not (fuse_o and C.decode_attn_oproj(q, kc, vc, sid32, clen32, attn.o_proj.weight, oacc, 1.0 / math.sqrt(D))):
+                o = ops.decode_attention(q, kc, vc, cache_len, sid32)
+                C.dgemv(0, o.reshape(M, nq * D), None, 0.0, attn.o_proj.weight, oacc[:M], 0, 0, 0, None, None, None, 1,
+                        None, None, None)                             # fp32 partial (overwrites)
+            ar.sum_(oacc[:M], osum[:M], zero_in=True)                 # osum = o_proj; oacc re-zeroed
+            a = torch.empty((M, w_d.shape[1]), dtype=res.dtype, device=res.device)
+            C.dgemv(2, res, ln2, self.eps, w_gu, a, 0, 0, 0, None, None, None, 1, None, None, None, osum, None)
+            C.dgemv(0, a, None, 0.0, w_d, dacc[:M], 0, 0, 0, None, None, None, 1, None, None, None)  # fp32 partial
+            ar.fold_residual_(dacc[:M], res, osum[:M])                # res += o_proj + down
+        h = res.view(B, T, -1)
+        if last_index is not None:
+            h = h[torch.arange(B, device=h.device), last_index]
+        h2 = h.reshape(-1, h.shape[-1]).contiguous()
+        logits = torch.empty((h2.shape[0], self.lm_head.weight.shape[0]), dtype=res.dtype, device=res.device)
+        C.dgemv(0, h2, self.model.norm.weight, self.eps, self.lm_head.weight, logits, 0, 0, 0, None, None, None, 1,
+                None, None, None)                                       # final norm + this rank's vocab slice
+        logits = self._gather_vocab(logits.view(h.shape[:-1] + (logits.shape[-1],)))
         if return_hidden:
             return logits, ops.rms_norm(h, self.model.norm.weight, self.eps)[0]
         return logits

@@ -1,0 +1,145 @@
+"""One-shot peer all-reduce for latency-bound tensor-parallel messages (csrc/peer_allreduce.hip).
+
+Tensor-parallel decode all-reduces a few KiB per row-parallel projection (o_proj, down: M x H fp32).
+Through RCCL each call is a ring of 2 (W - 1) link latencies plus a launch; here every rank exports one
+device region (its IPC handle exchanged once over the process group), maps every peer's, and ONE kernel
+per call publishes this rank's partial, waits for the peers' flags and sums all W partials in rank
+order -- identical bits on every rank, no host involvement, capturable in the decode hipGraph.
+
+Reference: the fork's TP decode compiles its all-reduces into one SPMD graph
+(examples/inference/modules/gqa.py:641-647, src/neuronx_distributed/trace/spmd.py:82-187).
+
+    par = PeerAllReduce(group, nmax=8 * hidden)
+    par.sum_(partial, out, zero_in=True)             # out = sum over ranks; partial zeroed
+    par.fold_residual_(partial, res, xadd)           # res = bf16(bf16(res + bf16(xadd)) + bf16(sum))
+    par.set_residual_(partial, res)                  # res = bf16(sum)
+
+`ProcessGroupAllReduce` has the same interface on torch.distributed (RCCL or gloo), the fallback when
+IPC is not available (CPU, or NXD_DECODE_PEER_AR=0).
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+SUM, FOLD_RES, SET_RES = 0, 1, 2
+
+
+class PeerAllReduce:
+    def __init__(self, group=None, nmax: int = 65536):
+        from ..ops._ext import ext
+
+        self.C = ext()
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if self.world > 8:
+            raise ValueError("peer all-reduce: at most 8 ranks (one node)")
+        self.nmax = int(nmax)
+        self.h = None
+        # every step is collective and every rank reaches every collective, so a failure on any rank
+        # (no IPC for this allocation, a handle that does not open) makes ALL ranks raise together
+        err = None
+        mine = None
+        try:
+            self.h, self.uncached = self.C.peer_ar_create(self.nmax)
+            mine = self.C.peer_ar_ipc_handle(self.h)
+        except Exception as e:
+            err = repr(e)
+        handles = [None] * self.world
+        dist.all_gather_object(handles, mine, group=group)
+        if err is None and all(h is not None for h in handles):
+            try:
+                self.C.peer_ar_open(self.h, self.rank, handles)
+            except Exception as e:
+                err = repr(e)
+        elif err is None:
+            err = "a peer could not export its buffer"
+        errs = [None] * self.world
+        dist.all_gather_object(errs, err, group=group)
+        bad = [e for e in errs if e is not None]
+        if bad:
+            self.close()
+            raise RuntimeError(f"peer all-reduce unavailable: {bad[0]}")
+
+    def _run(self, inp: torch.Tensor, zero_in: bool, mode: int, out=None, res=None, xadd=None):
+        if inp.numel() > self.nmax or inp.numel() % 4:
+            raise ValueError(f"peer all-reduce: {inp.numel()} elements (max {self.nmax}, multiple of 4)")
+        self.C.peer_ar_run(self.h, inp, zero_in, mode, out, res, xadd)
+
+    def sum_(self, inp: torch.Tensor, out: torch.Tensor, zero_in: bool = False) -> torch.Tensor:
+        self._run(inp, zero_in, SUM, out=out)
+        return out
+
+    def fold_residual_(self, inp: torch.Tensor, res: torch.Tensor, xadd: torch.Tensor, zero_in: bool = False):
+        self._run(inp, zero_in, FOLD_RES, res=res, xadd=xadd)
+        return res
+
+    def set_residual_(self, inp: torch.Tensor, res: torch.Tensor, zero_in: bool = False):
+        self._run(inp, zero_in, SET_RES, res=res)
+        return res
+
+    def error_count(self) -> int:
+        """Calls in which some peer never arrived within the bounded spin (0 when healthy)."""
+        return int(self.C.peer_ar_error(self.h))
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.C.peer_ar_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+
+class ProcessGroupAllReduce:
+    """The same operations on torch.distributed (RCCL graph-capturable; gloo host-staged)."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def sum_(self, inp: torch.Tensor, out: torch.Tensor, zero_in: bool = False) -> torch.Tensor:
+        dist.all_reduce(inp, group=self.group)
+        out.copy_(inp)
+        if zero_in:
+            inp.zero_()
+        return out
+
+    def fold_residual_(self, inp: torch.Tensor, res: torch.Tensor, xadd: torch.Tensor, zero_in: bool = False):
+        dist.all_reduce(inp, group=self.group)
+        y = (res.float() + xadd.reshape(res.shape).to(torch.bfloat16).float()).to(torch.bfloat16)
+        res.copy_((y.float() + inp.reshape(res.shape).to(torch.bfloat16).float()).to(torch.bfloat16))
+        if zero_in:
+            inp.zero_()
+        return res
+
+    def set_residual_(self, inp: torch.Tensor, res: torch.Tensor, zero_in: bool = False):
+        dist.all_reduce(inp, group=self.group)
+        res.copy_(inp.reshape(res.shape))
+        if zero_in:
+            inp.zero_()
+        return res
+
+    def error_count(self) -> int:
+        return 0
+
+    def close(self) -> None:
+        pass
+
+
+def make_decode_all_reduce(group, nmax: int, device: Optional[torch.device] = None, prefer_peer: bool = True):
+    """The peer all-reduce when IPC works on this node, else the process-group one."""
+    if prefer_peer and device is not None and torch.device(device).type == "cuda":
+        try:
+            return PeerAllReduce(group, nmax)
+        except Exception as e:  # no IPC (e.g. a runtime without it): fall back, loudly
+            from ..utils.logger import get_logger
+
+            get_logger().warning("peer all-reduce unavailable (%s); decode all-reduces go through the process group", e)
+    return ProcessGroupAllReduce(group)
