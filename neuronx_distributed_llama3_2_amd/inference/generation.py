@@ -297,6 +297,12 @@ class LlamaForCausalLMInference:
     def reset(self) -> None:
         self.kv_cache_populated = False
 
+    def set_fused_decode(self, enabled: bool) -> None:
+        """A/B switch of the fused decode kernels (csrc/decode_fused.hip, decode_attn.hip; at TP > 1 with
+        the one-shot peer all-reduce) against the unfused per-op decode; the next decode step re-checks
+        whether the model can take the fused path."""
+        self.model._decode_fused_ok = None if enabled else False
+
     def _context_encode(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                         position_ids: Optional[torch.Tensor] = None, seq_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Prefill; returns logits [B, V] of each sequence's last valid token (fp32)."""
