@@ -30,6 +30,7 @@ from .bucketing import pad_to_bucket
 from .config import InferenceConfig
 from .graphs import DecodeGraph, DecodeState, decode_step
 from .modeling_llama import LlamaInferenceModel
+from ..utils.graph_capture import graph_capture
 
 logger = get_logger()
 
@@ -88,7 +89,7 @@ class PrefillGraph:
         torch.cuda.current_stream(device).wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
         self.pool = pool if pool is not None else torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(self.graph, pool=self.pool):
+        with graph_capture(self.graph, pool=self.pool):
             self.out = self._fwd()
 
     def _fwd(self):

@@ -18,6 +18,7 @@ import torch
 
 from .. import ops
 from ..utils.sampling import Sampler
+from ..utils.graph_capture import graph_capture
 
 # greedy decoding ends each step with the fused argmax + feed-back launch pair (ops.greedy_advance_)
 GREEDY_FUSED = os.environ.get("NXD_GREEDY_FUSED", "1") == "1"
@@ -91,7 +92,7 @@ class DecodeGraph:
         for t, v in zip((st.tokens, st.positions, st.cache_len, st.step), saved):
             t.copy_(v)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with graph_capture(self.graph):
             self._run_eager()
         for t, v in zip((st.tokens, st.positions, st.cache_len, st.step), saved):
             t.copy_(v)

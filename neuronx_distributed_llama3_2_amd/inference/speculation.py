@@ -25,6 +25,7 @@ from typing import Optional
 import torch
 
 from ..ops.decode import argmax_rows
+from ..utils.graph_capture import graph_capture
 
 __all__ = ["SpeculativeDecoder", "SpecState", "spec_round"]
 
@@ -127,7 +128,7 @@ class SpeculativeDecoder:
             for t, v in zip(bufs, saved):
                 t.copy_(v)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with graph_capture(g):
                 self._run(st)
             for t, v in zip(bufs, saved):
                 t.copy_(v)

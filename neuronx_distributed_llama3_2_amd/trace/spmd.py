@@ -16,6 +16,7 @@ from __future__ import annotations
 from typing import Callable, Dict, List, Optional, Sequence
 
 import torch
+from ..utils.graph_capture import graph_capture
 
 
 def _shape_key(inputs: Sequence[torch.Tensor]) -> str:
@@ -39,7 +40,7 @@ class GraphRunner:
                     fn(*self.static_in)
             torch.cuda.current_stream().wait_stream(s)
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with graph_capture(self.graph):
                 self.static_out = fn(*self.static_in)
 
     def __call__(self, *inputs: torch.Tensor):

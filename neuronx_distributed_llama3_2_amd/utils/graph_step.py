@@ -19,6 +19,7 @@ from __future__ import annotations
 from typing import Callable, List, Sequence
 
 import torch
+from .graph_capture import graph_capture
 
 
 class GraphedTrainStep:
@@ -47,7 +48,7 @@ class GraphedTrainStep:
         torch.cuda.synchronize()
         self._restore(snap_params, snap_state, snap_step)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with graph_capture(self.graph):
             self.static_loss = self._step()
         torch.cuda.synchronize()
         # capture records without executing, but its host-side bookkeeping (step counter) advanced
