@@ -32,7 +32,7 @@ with torch.cuda.stream(s):
     x.add_(1)
 torch.cuda.synchronize()
 with torch.cuda.graph(h.g):
-    x.add_(1)
+    h.z = x * 3                            # the graph's private memory pool holds an allocation
 del h
 gc.enable()
 gc.set_threshold(50)
@@ -40,8 +40,9 @@ g2 = torch.cuda.CUDAGraph()
 ctx = graph_capture(g2) if {use_guard} else torch.cuda.graph(g2)
 with ctx:
     y = x * 2
-    for i in range(2000):                  # container allocations: trigger gen-0 collections
-        junk = [[i], {{"k": i}}]
+    keep = []
+    for i in range(5000):                  # live container allocations: trigger gen-0 collections
+        keep.append([i])
 g2.replay()
 torch.cuda.synchronize()
 print("capture ok")

@@ -9,6 +9,8 @@ export PYTHONUNBUFFERED=1
 PYT="python -u -m pytest -x -v -s --timeout 300 --timeout-method thread"
 timeout -k 10 400 $PYT tests/test_peer_allreduce_gpu.py -k "2" > $O/pytest_par.log 2>&1 || { tail -40 $O/pytest_par.log; exit 1; }
 grep -E "checks|passed|failed" $O/pytest_par.log
+timeout -k 10 300 $PYT tests/test_graph_capture_gpu.py > $O/pytest_gc.log 2>&1 || { tail -40 $O/pytest_gc.log; exit 1; }
+grep -E "PASS|FAIL" $O/pytest_gc.log
 timeout -k 10 900 $PYT tests/test_spmd_inference_gpu.py tests/test_inference_gpu.py > $O/pytest_inf.log 2>&1 || { tail -40 $O/pytest_inf.log; exit 1; }
 grep -E "near-tie|passed|failed" $O/pytest_inf.log
 A="--prompt 128 --new 256 --runs 5"
