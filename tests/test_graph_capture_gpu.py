@@ -4,8 +4,7 @@ another graph captures -> its destructor destroys a HIP graph during capture
 (hipErrorStreamCaptureUnsupported) -> std::terminate -> "Fatal Python error: Aborted ... Garbage-
 collecting".  torch.cuda.graph no longer collects at entry by default (torch 2.10:
 torch.compiler.config.force_cudagraph_gc), so a dead cycle from an earlier model survives into the
-next capture.  Each case runs in a child process (an abort must not take pytest down): plain
-torch.cuda.graph aborts, utils.graph_capture (cyclic GC held off during capture) completes."""
+next capture.  Runs in a child process (an abort must not take pytest down)."""
 import os
 import subprocess
 import sys
@@ -49,14 +48,13 @@ print("capture ok")
 '''
 
 
-@pytest.mark.parametrize("use_guard", [True, False])
-def test_gc_during_capture(use_guard):
-    code = SCRIPT.format(root=ROOT, use_guard=use_guard)
+def test_gc_during_capture_is_held_off():
+    """A dead graph (with pool memory) in a reference cycle plus enough live allocations inside the
+    capture to trigger collections: graph_capture completes and the captured graph replays.  (The
+    plain-torch.cuda.graph arm of this script did not abort on the box -- the destructor's failing HIP
+    call depends on the old graph's state -- so the evidence of the failure mode is the native stack
+    recorded in profiles/r5_decode_abort_native_backtrace.txt.)"""
+    code = SCRIPT.format(root=ROOT, use_guard=True)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
                        env=dict(os.environ, NXD_ABORT_BACKTRACE="1"))
-    if use_guard:
-        assert r.returncode == 0 and "capture ok" in r.stdout, r.stderr[-3000:]
-    else:
-        # the failure mode itself: without the guard the old graph's destructor runs mid-capture
-        assert r.returncode != 0, r.stdout
-        assert "CUDAGraph" in r.stderr or "capturing" in r.stderr, r.stderr[-3000:]
+    assert r.returncode == 0 and "capture ok" in r.stdout, r.stderr[-3000:]
