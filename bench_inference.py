@@ -31,7 +31,8 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--gloo-gpu", action="store_true",
                     help="TP rehearsal on a one-GPU box: every rank on cuda:0, gloo process group (the decode "
-                         "all-reduces still run the one-shot peer kernel over IPC); eager decode")
+                         "all-reduces and vocabulary gather run on the one-shot peer kernels over IPC, so decode is "
+                         "still captured in hipGraphs); prefill eager")
     ap.add_argument("--quantized", default=None, choices=[None, "per_tensor_symmetric", "per_channel_symmetric"])
     ap.add_argument("--report", default="gpurun_out/benchmark_report.json")
     ap.add_argument("--weight-layout", action="store_true",
@@ -43,8 +44,7 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         if args.gloo_gpu:
-            dist.init_process_group("gloo")
-            args.no_graphs = True   # gloo collectives (vocab gather) are host-staged: not capturable
+            dist.init_process_group("gloo")   # prefill eager; decode graphs when the peer kernels carry it
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from neuronx_distributed_llama3_2_amd.inference import InferenceConfig, LlamaForCausalLMInference

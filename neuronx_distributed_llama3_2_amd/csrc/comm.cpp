@@ -29,7 +29,7 @@ int multi_copy_launch(const void* const*, void* const*, const int64_t*, int, hip
 void* peer_ar_create(int, int*);
 int peer_ar_ipc_handle(void*, void*);
 int peer_ar_open(void*, int, int, const void*);
-int peer_ar_run(void*, float*, int, int, int, float*, void*, const float*, hipStream_t);
+int peer_ar_run(void*, float*, int, int, int, float*, void*, const float*, int, hipStream_t);
 int peer_ar_error(void*);
 void peer_ar_destroy(void*);
 }
@@ -346,8 +346,23 @@ void peer_ar_run(int64_t h, at::Tensor in, bool zero_in, int64_t mode, c10::opti
     xp = xadd->data_ptr<float>();
   }
   const int rc = nxd::peer_ar_run(reinterpret_cast<void*>(h), in.data_ptr<float>(), zero_in ? 1 : 0, (int)mode, (int)n, op,
-                                  rp, xp, at::hip::getCurrentHIPStream().stream());
+                                  rp, xp, 0, at::hip::getCurrentHIPStream().stream());
   TORCH_CHECK(rc == 0, "peer all-reduce: launch failed (", rc, ")");
+}
+
+// all-gather of [rows, C] slices (any dtype; row bytes a multiple of 16) into [rows, world * C]
+void peer_ar_gather(int64_t h, at::Tensor in, at::Tensor out, int64_t world) {
+  TORCH_CHECK(in.is_cuda() && in.is_contiguous() && out.is_contiguous() && in.dim() == 2 && out.dim() == 2 &&
+                  in.scalar_type() == out.scalar_type(),
+              "peer gather: contiguous 2-D tensors of one dtype");
+  const int64_t row_bytes = in.size(1) * in.element_size();
+  TORCH_CHECK(row_bytes % 16 == 0 && out.size(0) == in.size(0) && out.size(1) == world * in.size(1),
+              "peer gather: row bytes % 16, out [rows, world * C]");
+  const int64_t nbytes = in.numel() * in.element_size();
+  const int rc = nxd::peer_ar_run(reinterpret_cast<void*>(h), reinterpret_cast<float*>(in.data_ptr()), 0, 3,
+                                  (int)(nbytes / 4), reinterpret_cast<float*>(out.data_ptr()), nullptr, nullptr,
+                                  (int)(row_bytes / 16), at::hip::getCurrentHIPStream().stream());
+  TORCH_CHECK(rc == 0, "peer gather: launch failed (", rc, ")");
 }
 
 std::string version() {
@@ -377,6 +392,7 @@ void register_comm(pybind11::module& m) {
   m.def("peer_ar_run", &peer_ar_run, pybind11::arg("h"), pybind11::arg("inp"), pybind11::arg("zero_in"),
         pybind11::arg("mode"), pybind11::arg("out") = pybind11::none(), pybind11::arg("res") = pybind11::none(),
         pybind11::arg("xadd") = pybind11::none());
+  m.def("peer_ar_gather", &peer_ar_gather);
   m.def("peer_ar_error", [](int64_t h) { return nxd::peer_ar_error(reinterpret_cast<void*>(h)); });
   m.def("peer_ar_destroy", [](int64_t h) { nxd::peer_ar_destroy(reinterpret_cast<void*>(h)); });
 }

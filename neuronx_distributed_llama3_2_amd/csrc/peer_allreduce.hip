@@ -36,7 +36,7 @@ constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 64;
 constexpr int kThreads = 256;
 
-enum Mode { SUM = 0, FOLD_RES = 1, SET_RES = 2 };
+enum Mode { SUM = 0, FOLD_RES = 1, SET_RES = 2, GATHER = 3 };
 
 struct Args {
   float* in;                                 // local partial [n] fp32
@@ -52,6 +52,9 @@ struct Args {
   float* out;                                // SUM: [n] fp32
   uint16_t* res;                             // FOLD_RES / SET_RES: bf16 residual stream [n]
   const float* xadd;                         // FOLD_RES: pending fp32 sum folded first (o_proj)
+  // GATHER: every rank's slice [rows][rowu x 16 B] (any dtype, moved as bytes) into
+  // out [rows][world][rowu x 16 B] -- the vocab-parallel logits of TP decode
+  int rowu;
 };
 
 __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
@@ -104,6 +107,22 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  if (a.mode == GATHER) {
+    // 16-byte units u of this block's chunk: row m = u / rowu, unit j = u % rowu of rank r's slice
+    const int u0 = lo / 4, u1 = hi / 4;
+    for (int u = u0 + tid; u < u1; u += kThreads) {
+      const int m = u / a.rowu, j = u - m * a.rowu;
+#pragma unroll
+      for (int r = 0; r < kMaxRanks; ++r) {
+        if (r < a.world) {
+          const u32x4_t v = reinterpret_cast<const u32x4_t*>(par ? a.peer_slot[r][1] : a.peer_slot[r][0])[u];
+          reinterpret_cast<u32x4_t*>(a.out)[((int64_t)m * a.world + r) * a.rowu + j] = v;
+        }
+      }
+    }
+    if (tid == 0) a.ctr[b] = e;
+    return;
+  }
   for (int i = lo + tid; i < hi; i += kThreads) {
     float s = 0.f;
 #pragma unroll
@@ -212,10 +231,12 @@ int peer_ar_open(void* hv, int world, int rank, const void* handles) {
 }
 
 int peer_ar_run(void* hv, float* in, int zero_in, int mode, int n, float* out, void* res, const float* xadd,
-                hipStream_t stream) {
+                int rowu, hipStream_t stream) {
   auto* h = static_cast<par::Handle*>(hv);
   if (n < 1 || n > h->nmax || h->world < 1) return -1;
-  if ((mode == par::SUM && !out) || (mode != par::SUM && !res) || (mode == par::FOLD_RES && !xadd)) return -2;
+  if (((mode == par::SUM || mode == par::GATHER) && !out) || ((mode == par::FOLD_RES || mode == par::SET_RES) && !res) ||
+      (mode == par::FOLD_RES && !xadd) || (mode == par::GATHER && (rowu < 1 || (n / 4) % rowu)))
+    return -2;
   if ((reinterpret_cast<uintptr_t>(in) & 15) || n % 4) return -3;
   par::Args a{};
   a.in = in;
@@ -245,6 +266,7 @@ int peer_ar_run(void* hv, float* in, int zero_in, int mode, int n, float* out, v
   a.out = out;
   a.res = static_cast<uint16_t*>(res);
   a.xadd = xadd;
+  a.rowu = rowu;
   hipLaunchKernelGGL(par::peer_allreduce_kernel, dim3(blocks), dim3(par::kThreads), 0, stream, a);
   return (int)hipGetLastError();
 }

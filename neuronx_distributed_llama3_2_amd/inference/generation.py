@@ -341,6 +341,15 @@ class LlamaForCausalLMInference:
                 return False
         return True
 
+    def _decode_graphs_allowed(self) -> bool:
+        """Decode graphs: as `_graphs_allowed`, and also on a gloo TP group when every collective of
+        the decode step runs on the one-shot peer kernels (model_base.peer_decode_ready)."""
+        if self._graphs_allowed():
+            return True
+        if not getattr(self.config, "use_hip_graphs", True) or self.device.type != "cuda":
+            return False
+        return getattr(self.config, "tp_degree", 1) > 1 and self.model.peer_decode_ready()
+
     def _prefill_graphs_on(self) -> bool:
         return getattr(self.config, "prefill_graphs", True) and self._graphs_allowed()
 
@@ -392,7 +401,7 @@ class LlamaForCausalLMInference:
         g = self._graphs.get(key)
         if g is None:
             g = self._graphs[key] = DecodeGraph(self.model, sampler, self._decode_state(batch), self.graph_steps,
-                                                use_graph=self._graphs_allowed())
+                                                use_graph=self._decode_graphs_allowed())
         return g
 
     @torch.no_grad()

@@ -252,6 +252,20 @@ class DecoderInferenceMixin:
             return logits, ops.rms_norm(h, self.model.norm.weight, self.eps)[0]
         return logits
 
+    def peer_decode_ready(self) -> bool:
+        """True when decode at TP > 1 runs entirely on the one-shot peer kernels (fused path, every
+        all-reduce and the vocabulary gather over IPC): no process-group collective is left in a decode
+        step, so it can be captured in a hipGraph even when the TP group itself is gloo (ranks sharing
+        one GPU).  Collective on first use (every rank calls it at the same point)."""
+        from ..parallel.peer_allreduce import PeerAllReduce
+
+        if self.tp == 1 or not self._check_decode_fusable():
+            return False
+        ew = self.model.embed_tokens.weight
+        if ew.device.type != "cuda":
+            return False
+        return isinstance(self._decode_tp_state(ew.shape[1], ew.device)["ar"], PeerAllReduce)
+
     def _decode_tp_state(self, H: int, device):
         """TP > 1 fused decode: fp32 [8, H] partial / sum buffers and the decode all-reduce (one-shot
         peer all-reduce over IPC when available -- parallel/peer_allreduce.py -- else the process
@@ -260,7 +274,8 @@ class DecoderInferenceMixin:
         if st is None or st["H"] != H or st["device"] != device:
             from ..parallel.peer_allreduce import make_decode_all_reduce
 
-            ar = make_decode_all_reduce(ps.get_tensor_model_parallel_group(), 8 * H, device,
+            vl = self.lm_head.weight.shape[0]   # this rank's vocabulary rows (bf16 logits gathered as bytes)
+            ar = make_decode_all_reduce(ps.get_tensor_model_parallel_group(), max(8 * H, 4 * vl), device,
                                         prefer_peer=os.environ.get("NXD_DECODE_PEER_AR", "1") == "1")
             z = lambda: torch.zeros((8, H), dtype=torch.float32, device=device)  # noqa: E731
             st = self._tp_dec = {"H": H, "device": device, "ar": ar, "oacc": z(), "osum": z(), "dacc": z(), "emb": z()}
@@ -321,7 +336,9 @@ class DecoderInferenceMixin:
         logits = torch.empty((h2.shape[0], self.lm_head.weight.shape[0]), dtype=res.dtype, device=res.device)
         C.dgemv(0, h2, self.model.norm.weight, self.eps, self.lm_head.weight, logits, 0, 0, 0, None, None, None, 1,
                 None, None, None)                                       # final norm + this rank's vocab slice
-        logits = self._gather_vocab(logits.view(h.shape[:-1] + (logits.shape[-1],)))
+        full = torch.empty((logits.shape[0], self.tp * logits.shape[1]), dtype=logits.dtype, device=logits.device)
+        ar.gather_(logits, full)                                        # vocab-parallel slices side by side
+        logits = full.view(h.shape[:-1] + (full.shape[-1],))
         if return_hidden:
             return logits, ops.rms_norm(h, self.model.norm.weight, self.eps)[0]
         return logits

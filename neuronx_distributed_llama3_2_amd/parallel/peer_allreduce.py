@@ -13,6 +13,7 @@ Reference: the fork's TP decode compiles its all-reduces into one SPMD graph
     par.sum_(partial, out, zero_in=True)             # out = sum over ranks; partial zeroed
     par.fold_residual_(partial, res, xadd)           # res = bf16(bf16(res + bf16(xadd)) + bf16(sum))
     par.set_residual_(partial, res)                  # res = bf16(sum)
+    par.gather_(logits_slice, logits_full)           # [rows, C] per rank -> [rows, world * C]
 
 `ProcessGroupAllReduce` has the same interface on torch.distributed (RCCL or gloo), the fallback when
 IPC is not available (CPU, or NXD_DECODE_PEER_AR=0).
@@ -82,6 +83,14 @@ class PeerAllReduce:
         self._run(inp, zero_in, SET_RES, res=res)
         return res
 
+    def gather_(self, inp: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """out [rows, world * C] = every rank's inp [rows, C] side by side (rank order); any dtype with
+        16-byte rows (the vocab-parallel decode logits)."""
+        if inp.numel() * inp.element_size() // 4 > self.nmax:
+            raise ValueError("peer gather: slice larger than the exported region")
+        self.C.peer_ar_gather(self.h, inp, out, self.world)
+        return out
+
     def error_count(self) -> int:
         """Calls in which some peer never arrived within the bounded spin (0 when healthy)."""
         return int(self.C.peer_ar_error(self.h))
@@ -125,6 +134,12 @@ class ProcessGroupAllReduce:
         if zero_in:
             inp.zero_()
         return res
+
+    def gather_(self, inp: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        parts = [torch.empty_like(inp) for _ in range(dist.get_world_size(self.group))]
+        dist.all_gather(parts, inp.contiguous(), group=self.group)
+        out.copy_(torch.cat(parts, dim=-1))
+        return out
 
     def error_count(self) -> int:
         return 0

@@ -53,6 +53,14 @@ def main():
             par.set_residual_(inp, res)
             assert torch.equal(res, want.to(torch.bfloat16)), it
         checks += 1
+    # the vocab-parallel logits gather (bf16 bytes, rank order)
+    for it in range(6):
+        rows, C = 1 + it % 4, 1000 + 8 * it
+        sl = [partial(900 + it, r, rows * C).to(torch.bfloat16).view(rows, C) for r in range(world)]
+        out = torch.empty(rows, world * C, dtype=torch.bfloat16, device="cuda")
+        par.gather_(sl[rank].clone(), out)
+        assert torch.equal(out, torch.cat(sl, dim=1)), it
+        checks += 1
     # inside a hipGraph: 4 calls per replay (an even and an odd count of calls between replays)
     n = 2048
     sin = torch.zeros(4, n, device="cuda")

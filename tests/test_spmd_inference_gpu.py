@@ -166,3 +166,28 @@ def test_tp2_fused_decode_matches_unfused_like_tp1():
         # 87.5 % of the greedy picks, so agreement is reported, not asserted)
         print(f"TP={tp}: fused vs unfused decode logits rel_l2 {rel[tp]:.5f}, greedy agreement {agree:.3f}")
     assert rel[2] <= 2 * rel[1] + 2e-3, rel
+
+
+def test_tp2_decode_hipgraph_on_peer_kernels():
+    """TP = 2 over a gloo group (two ranks sharing the GPU): with every decode collective on the
+    one-shot peer kernels (all-reduces and the vocabulary gather over IPC) the decode loop is captured
+    in hipGraphs, and its greedy tokens equal the eager TP = 2 decode's."""
+    from neuronx_distributed_llama3_2_amd.inference.spmd_server import SpmdGenerationServer
+
+    cfg = _cfg("tiny")
+    d = tempfile.mkdtemp()
+    path = os.path.join(d, "full.pt")
+    torch.save(_random_full_state(cfg, "tiny", seed=4), path)
+    torch.manual_seed(11)
+    ids = torch.randint(3, cfg.vocab_size, (2, 16))
+    outs = {}
+    for graphs in (True, False):
+        kw = dict(batch_size=2, seq_len=128, max_context_length=96, deterministic=True, use_hip_graphs=graphs,
+                  decode_graph_steps=8)
+        server = SpmdGenerationServer.from_full_state_dict(cfg.to_dict(), path, 2, kw, dtype="bfloat16")
+        try:
+            assert server.pool.call("_decode_graphs_allowed") is graphs
+            outs[graphs] = server.generate(ids, max_new_tokens=40, eos_token_id=-1)
+        finally:
+            server.close()
+    assert torch.equal(outs[True], outs[False])
