@@ -13,3 +13,5 @@ grep -E "TP=|near-tie|first differing|passed|failed" $O/pytest_spmd.log
 A="--prompt 128 --new 256 --runs 5"
 timeout -k 10 400 python -u tools/experiments/r5/launch_ranks.py 2 -- python -u bench_inference.py $A --gloo-gpu --report $O/tp2_gloo_gpu_graphs.json > $O/tp2.log 2>&1 || { tail -20 $O/tp2.log; exit 1; }
 python -c "import json; d=json.load(open('$O/tp2_gloo_gpu_graphs.json')); print('tp2 graphs', d['token_generation'], d['config']['hip_graphs'])"
+timeout -k 10 300 python -u tools/bench_dense_vs_hipblaslt.py > $O/dense_vs_hipblaslt.jsonl 2>$O/dense.err || { tail -20 $O/dense.err; exit 1; }
+cat $O/dense_vs_hipblaslt.jsonl
