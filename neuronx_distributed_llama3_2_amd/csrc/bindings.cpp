@@ -20,6 +20,7 @@ int flash_attn_fwd_launch(const void*, const void*, const void*, void*, float*, 
 int64_t flash_attn_bwd_workspace(int, int, int, int, int, int, int, int);
 void flash_attn_bwd_set_knob(int, int);
 int transpose_bf16_launch(const void*, void*, int64_t, int64_t, int64_t, int64_t, hipStream_t);
+void transpose_set_variant(int);
 int flash_attn_bwd_launch(const void*, const void*, const void*, const void*, const void*, const float*, float*,
                           void*, void*, void*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                           const int64_t*, const int64_t*, const int64_t*, const int64_t*, int, int, int, int, int, int,
@@ -1078,6 +1079,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("flash_attn_set_knob", [](int which, int value) { nxd::flash_attn_bwd_set_knob(which, value); });
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("transpose_set_variant", [](bool tr) { nxd::transpose_set_variant(tr ? 1 : 0); });
   m.def("rmsnorm_set_rows_path", [](bool on) { nxd::rmsnorm_set_rows_path(on ? 1 : 0); });
   m.def("rope_inplace", &rope_inplace);
   m.def("swiglu_fwd", &swiglu_fwd);

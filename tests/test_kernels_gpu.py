@@ -480,13 +480,23 @@ def test_argmax_large_vocab():
     assert a.tolist() == [int(x[0].float().argmax()), 77777, 5]
 
 
-@pytest.mark.parametrize("R,C", [(64, 64), (8192, 4096), (1000, 72), (4096, 14336)])
-def test_transpose_bf16(R, C):
+@pytest.mark.parametrize("tr", [True, False])
+@pytest.mark.parametrize("R,C", [(64, 64), (8, 8), (8192, 4096), (1000, 72), (72, 1000), (4096, 14336), (136, 8200)])
+def test_transpose_bf16(R, C, tr):
+    """Both transpose kernels (csrc/transpose.hip: ds_read_b64_tr_b16 tile, and the 16-bit LDS one)
+    bit-exact against torch, with partial edge tiles and a source row stride wider than C."""
+    from neuronx_distributed_llama3_2_amd import _C
     from neuronx_distributed_llama3_2_amd.ops import gemm
 
-    x = torch.randn(R + 8, C, device=DEV, dtype=torch.bfloat16)[:R]   # padded row stride too
-    y = gemm.transpose(x)
-    assert torch.equal(y, x.t().contiguous())
+    _C.transpose_set_variant(tr)
+    try:
+        x = torch.randn(R, C + 8, device=DEV, dtype=torch.bfloat16)[:, :C]   # row stride C + 8
+        y = gemm.transpose(x)
+        assert torch.equal(y, x.t().contiguous())
+        x2 = torch.randn(R, C, device=DEV, dtype=torch.bfloat16)
+        assert torch.equal(gemm.transpose(x2), x2.t().contiguous())
+    finally:
+        _C.transpose_set_variant(True)
 
 
 def test_dgrad_kmajor_weight_refreshes():
