@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(256) transpose_tr_kernel(const uint16_t* __res
   }
 }
 
-static int g_v2 = -1;   // NXD_TRANSPOSE_TR (default 1); transpose_set_variant for in-process A/B
+static int g_v2 = -1;   // NXD_TRANSPOSE_TR (default 0); transpose_set_variant for in-process A/B
 
 }  // namespace tr
 
@@ -116,7 +116,7 @@ int transpose_bf16_launch(const void* src, void* dst, int64_t R, int64_t C, int6
   if (grid.y > 65535) return -2;
   if (tr::g_v2 < 0) {
     const char* e = getenv("NXD_TRANSPOSE_TR");
-    tr::g_v2 = e ? (atoi(e) != 0) : 1;
+    tr::g_v2 = e ? (atoi(e) != 0) : 0;   // opt-in: 5.2 vs 5.7 TB/s at 8192 x 4096 (profiles/r5_transpose_tr_vs_lds16.jsonl)
   }
   if (tr::g_v2)
     hipLaunchKernelGGL(tr::transpose_tr_kernel, grid, dim3(256), 0, stream, (const uint16_t*)src, (uint16_t*)dst, R,
