@@ -26,7 +26,8 @@
 namespace nxd {
 int multi_copy_launch(const void* const*, void* const*, const int64_t*, int, hipStream_t);
 // peer_allreduce.hip: one-shot all-reduce over IPC-mapped peer buffers
-void* peer_ar_create(int, int*);
+void* peer_ar_create(int64_t, int*);
+int peer_coll_run(void*, const void*, void*, int64_t, int, int, hipStream_t);
 int peer_ar_ipc_handle(void*, void*);
 int peer_ar_open(void*, int, int, const void*);
 int peer_ar_run(void*, float*, int, int, int, float*, void*, const float*, int, hipStream_t);
@@ -304,7 +305,7 @@ int64_t bucketed_all_reduce(int64_t h, std::vector<at::Tensor> ts, at::Tensor st
 // res = bf16(bf16(res + bf16(xadd)) + bf16(sum)), 2 res = bf16(sum).
 pybind11::tuple peer_ar_create(int64_t nmax) {
   int unc = 0;
-  void* h = nxd::peer_ar_create((int)nmax, &unc);
+  void* h = nxd::peer_ar_create(nmax, &unc);
   TORCH_CHECK(h, "peer all-reduce: device allocation failed");
   return pybind11::make_tuple(reinterpret_cast<int64_t>(h), unc != 0);
 }
@@ -350,6 +351,20 @@ void peer_ar_run(int64_t h, at::Tensor in, bool zero_in, int64_t mode, c10::opti
   TORCH_CHECK(rc == 0, "peer all-reduce: launch failed (", rc, ")");
 }
 
+// sequence-parallel all-gather (mode 0: out = [world * n]) / reduce-scatter (mode 1: in = [world * n])
+void peer_coll(int64_t h, at::Tensor in, at::Tensor out, int64_t mode) {
+  TORCH_CHECK(in.is_cuda() && in.is_contiguous() && out.is_contiguous() && in.scalar_type() == out.scalar_type(),
+              "peer collective: contiguous GPU tensors of one dtype");
+  TORCH_CHECK(in.scalar_type() == at::kBFloat16 || in.scalar_type() == at::kFloat || mode == 0,
+              "peer reduce-scatter: bf16 or fp32");
+  const int es = (int)in.element_size();
+  TORCH_CHECK(es == 2 || es == 4, "peer collective: 2- or 4-byte elements");
+  const int64_t n = mode == 0 ? in.numel() : out.numel();
+  const int rc = nxd::peer_coll_run(reinterpret_cast<void*>(h), in.data_ptr(), out.data_ptr(), n, es, (int)mode,
+                                    at::hip::getCurrentHIPStream().stream());
+  TORCH_CHECK(rc == 0, "peer collective: launch failed (", rc, ")");
+}
+
 // all-gather of [rows, C] slices (any dtype; row bytes a multiple of 16) into [rows, world * C]
 void peer_ar_gather(int64_t h, at::Tensor in, at::Tensor out, int64_t world) {
   TORCH_CHECK(in.is_cuda() && in.is_contiguous() && out.is_contiguous() && in.dim() == 2 && out.dim() == 2 &&
@@ -393,6 +408,7 @@ void register_comm(pybind11::module& m) {
         pybind11::arg("mode"), pybind11::arg("out") = pybind11::none(), pybind11::arg("res") = pybind11::none(),
         pybind11::arg("xadd") = pybind11::none());
   m.def("peer_ar_gather", &peer_ar_gather);
+  m.def("peer_coll", &peer_coll);
   m.def("peer_ar_error", [](int64_t h) { return nxd::peer_ar_error(reinterpret_cast<void*>(h)); });
   m.def("peer_ar_destroy", [](int64_t h) { nxd::peer_ar_destroy(reinterpret_cast<void*>(h)); });
 }

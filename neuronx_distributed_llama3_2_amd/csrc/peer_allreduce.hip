@@ -8,7 +8,8 @@
 // reads all W partials directly: ONE kernel launch per all-reduce, no host involvement, capturable in
 // the decode hipGraph.
 //
-// Per rank, one IPC-exported region: flags [2][kMaxBlocks] (uint64 epochs) + slots [2][nmax] fp32.
+// Per rank, one IPC-exported region: a 4 KiB header of flags [2][kMaxBlocks] (uint64 epochs) + slots
+// [2][nmax x 4 B].
 // Call c of a rank has epoch e = ctr[b] + 1 (per-block device counter, so hipGraph replays keep
 // counting) and parity e & 1.  Block b of every rank:
 //   1. copies its chunk of the local partial into slot[parity] (and zeroes the partial when it is an
@@ -33,7 +34,7 @@ namespace nxd {
 namespace par {
 
 constexpr int kMaxRanks = 8;
-constexpr int kMaxBlocks = 64;
+constexpr int kMaxBlocks = 128;
 constexpr int kThreads = 256;
 
 enum Mode { SUM = 0, FOLD_RES = 1, SET_RES = 2, GATHER = 3 };
@@ -144,7 +145,7 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
 struct Handle {
   char* base = nullptr;        // IPC region: flags, slot 0, slot 1
   size_t bytes = 0;
-  int nmax = 0;
+  int64_t nmax = 0;
   bool uncached = false;
   int world = 0, rank = 0;
   char* peer_base[kMaxRanks] = {};
@@ -154,21 +155,129 @@ struct Handle {
 };
 
 constexpr size_t kFlagBytes = 2 * kMaxBlocks * sizeof(uint64_t);
+constexpr size_t kHeader = 4096;
 
-size_t slot_offset(int nmax, int s) {
+size_t slot_offset(int64_t nmax, int s) {
   const size_t slot_bytes = ((size_t)nmax * 4 + 255) / 256 * 256;
-  return 1024 + (size_t)s * slot_bytes;
+  return kHeader + (size_t)s * slot_bytes;
+}
+
+// ---- bandwidth-class collectives on the same region: all-gather and reduce-scatter of the
+// sequence-parallel activations (a ring uses one xGMI link per hop; here every rank
+// reads each peer's slot directly, all 7 links of a node at once).  Same epoch / parity / publish /
+// wait protocol as peer_allreduce_kernel; elements per rank n and per block `chunk` are multiples
+// of 8.  AG: out[r n + i] = in_r[i] (bytes).  RS: out[i] = sum_r in_r[rank n + i] (fp32 accumulate
+// in rank order, bf16 or fp32 io).
+struct CollArgs {
+  const char* in;
+  char* slot[2];
+  const char* peer_slot[kMaxRanks][2];
+  uint64_t* flag;
+  const uint64_t* peer_flag[kMaxRanks];
+  uint64_t* ctr;
+  int* err;
+  int world, rank, es, mode;   // es: element bytes (2 | 4); mode 0 AG, 1 RS
+  int64_t n, chunk, spin_limit;
+  char* out;
+};
+
+__device__ __forceinline__ void copy16(const char* src, char* dst, int64_t b0, int64_t b1, int tid) {
+  for (int64_t o = b0 + (int64_t)tid * 16; o < b1; o += (int64_t)kThreads * 16)
+    *reinterpret_cast<u32x4_t*>(dst + o) = *reinterpret_cast<const u32x4_t*>(src + o);
+}
+
+__global__ void __launch_bounds__(kThreads) peer_coll_kernel(CollArgs a) {
+  __shared__ uint64_t e_s;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int64_t lo = (int64_t)b * a.chunk, hi = min(a.n, lo + a.chunk);
+  if (tid == 0) e_s = a.ctr[b] + 1;
+  __syncthreads();
+  const uint64_t e = e_s;
+  const int par = (int)(e & 1);
+  char* mine = a.slot[par];
+  if (a.mode == 0) {
+    copy16(a.in, mine, lo * a.es, hi * a.es, tid);
+  } else {
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r)
+      if (r < a.world) copy16(a.in, mine, ((int64_t)r * a.n + lo) * a.es, ((int64_t)r * a.n + hi) * a.es, tid);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(a.flag + par * kMaxBlocks + b, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const uint64_t* pf = nullptr;
+#pragma unroll
+  for (int r = 0; r < kMaxRanks; ++r)
+    if (r == tid) pf = a.peer_flag[r] + par * kMaxBlocks + b;
+  if (tid < a.world && tid != a.rank) {
+    int64_t it = 0;
+    while (__hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > a.spin_limit) {
+        atomicAdd(a.err, 1);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (a.mode == 0) {
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r) {
+      if (r < a.world) {
+        const char* src = par ? a.peer_slot[r][1] : a.peer_slot[r][0];
+        for (int64_t o = lo * a.es + (int64_t)tid * 16; o < hi * a.es; o += (int64_t)kThreads * 16)
+          *reinterpret_cast<u32x4_t*>(a.out + (int64_t)r * a.n * a.es + o) = *reinterpret_cast<const u32x4_t*>(src + o);
+      }
+    }
+  } else {
+    const int64_t base = (int64_t)a.rank * a.n;
+    const int per = 16 / a.es;   // elements per 16-byte vector
+    for (int64_t i = lo + (int64_t)tid * per; i < hi; i += (int64_t)kThreads * per) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < kMaxRanks; ++r) {
+        if (r < a.world) {
+          const char* src = par ? a.peer_slot[r][1] : a.peer_slot[r][0];
+          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(src + (base + i) * a.es);
+          if (a.es == 2) {
+            float f[8];
+            unpack8(v, f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] += f[j];
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] += __uint_as_float(v[j]);
+          }
+        }
+      }
+      if (a.es == 2) {
+        *reinterpret_cast<u32x4_t*>(a.out + i * 2) = pack8(acc);
+      } else {
+        *reinterpret_cast<f32x4_t*>(a.out + i * 4) = f32x4_t{acc[0], acc[1], acc[2], acc[3]};
+      }
+    }
+  }
+  if (tid == 0) a.ctr[b] = e;
 }
 
 }  // namespace par
 
 // ---- host API (comm.cpp binds it) ----------------------------------------------------------------
 
-void* peer_ar_create(int nmax, int* uncached) {
+void* peer_ar_create(int64_t nmax, int* uncached) {
   auto* h = new par::Handle();
   h->nmax = nmax;
   h->bytes = par::slot_offset(nmax, 2);
-  static_assert(par::kFlagBytes <= 1024, "flag block");
+  static_assert(par::kFlagBytes <= par::kHeader, "flag block");
   // fine-grained, uncached device memory: coherent for peers on other GPUs without relying on cache
   // maintenance; plain device memory if the runtime cannot export such an allocation
   void* p = nullptr;
@@ -268,6 +377,43 @@ int peer_ar_run(void* hv, float* in, int zero_in, int mode, int n, float* out, v
   a.xadd = xadd;
   a.rowu = rowu;
   hipLaunchKernelGGL(par::peer_allreduce_kernel, dim3(blocks), dim3(par::kThreads), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+// AG (mode 0): in [n] -> out [world * n]; RS (mode 1): in [world * n] -> out [n]; es = 2 (bf16) or 4 (fp32)
+int peer_coll_run(void* hv, const void* in, void* out, int64_t n, int es, int mode, hipStream_t stream) {
+  auto* h = static_cast<par::Handle*>(hv);
+  if (h->world < 1 || n < 1 || n % 8 || (es != 2 && es != 4) || (mode != 0 && mode != 1)) return -1;
+  const int64_t need = (mode == 0 ? n : (int64_t)h->world * n) * es;
+  if (need > (int64_t)h->nmax * 4) return -2;
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return -3;
+  par::CollArgs a{};
+  a.in = static_cast<const char*>(in);
+  for (int s = 0; s < 2; ++s) a.slot[s] = h->base + par::slot_offset(h->nmax, s);
+  for (int r = 0; r < h->world; ++r) {
+    for (int s = 0; s < 2; ++s) a.peer_slot[r][s] = h->peer_base[r] + par::slot_offset(h->nmax, s);
+    a.peer_flag[r] = reinterpret_cast<const uint64_t*>(h->peer_base[r]);
+  }
+  a.flag = reinterpret_cast<uint64_t*>(h->base);
+  a.ctr = h->ctr;
+  a.err = h->err;
+  a.world = h->world;
+  a.rank = h->rank;
+  a.es = es;
+  a.mode = mode;
+  a.n = n;
+  // 64 KiB of this rank's elements per block (latency-bound below that), at most kMaxBlocks blocks
+  int64_t blocks = (n * es + 65535) / 65536;
+  blocks = blocks < 1 ? 1 : (blocks > par::kMaxBlocks ? par::kMaxBlocks : blocks);
+  a.chunk = ((n + blocks - 1) / blocks + 7) / 8 * 8;
+  blocks = (n + a.chunk - 1) / a.chunk;
+  static const int64_t limit = [] {
+    const char* e = getenv("NXD_PEER_AR_SPIN_LIMIT");
+    return e ? atoll(e) : (int64_t)1 << 24;
+  }();
+  a.spin_limit = limit;
+  a.out = static_cast<char*>(out);
+  hipLaunchKernelGGL(par::peer_coll_kernel, dim3((unsigned)blocks), dim3(par::kThreads), 0, stream, a);
   return (int)hipGetLastError();
 }
 

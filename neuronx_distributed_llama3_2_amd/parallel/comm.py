@@ -143,6 +143,28 @@ def _native_for(group, t: torch.Tensor):
     return c
 
 
+# NXD_SP_PEER=1: all-gather / reduce-scatter of GPU tensors (the sequence-parallel activations) over
+# IPC-mapped peer buffers, one kernel per call reading every peer directly
+# (parallel/peer_allreduce.py PeerCollectives; any group backend, so ranks sharing one GPU over gloo
+# run it too).  Off by default: not yet measured across GPUs.
+_peer = os.environ.get("NXD_SP_PEER", "0") == "1"
+_peer_colls: Dict[object, object] = {}
+
+
+def _peer_for(group, t: torch.Tensor, op=None):
+    if not _peer or not t.is_cuda or (op is not None and op != dist.ReduceOp.SUM):
+        return None
+    if t.element_size() not in (2, 4) or (t.numel() * t.element_size()) % 16:
+        return None
+    key = group if group is not None else "world"
+    c = _peer_colls.get(key)
+    if c is None:
+        from .peer_allreduce import PeerCollectives
+
+        c = _peer_colls[key] = PeerCollectives(group)
+    return c
+
+
 def _native_result(work, async_op: bool, op: str, t: torch.Tensor):
     if not async_op:
         return None
@@ -159,6 +181,10 @@ def _is_gloo(group) -> bool:
 def all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
     """out[i*n:(i+1)*n] = inp of rank i (dim 0)."""
     _fr("all_gather", out, group)
+    pc = _peer_for(group, inp)
+    if pc is not None and (inp.numel() % 8 == 0):
+        w = pc.all_gather(out, inp, async_op=async_op)
+        return _track(w, "all_gather", out) if async_op else None
     nc = _native_for(group, out)
     if nc is not None:
         return _native_result(nc.all_gather([out], [inp.contiguous()], async_op=async_op), async_op, "all_gather", out)
@@ -179,6 +205,10 @@ def reduce_scatter_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, asyn
                           op=dist.ReduceOp.SUM):
     """out = sum over ranks of inp[rank*n:(rank+1)*n] (dim 0)."""
     _fr("reduce_scatter", inp, group)
+    pc = _peer_for(group, inp, op)
+    if pc is not None and out.numel() % 8 == 0 and inp.dtype in (torch.bfloat16, torch.float32):
+        w = pc.reduce_scatter(out, inp, async_op=async_op)
+        return _track(w, "reduce_scatter", inp) if async_op else None
     nc = _native_for(group, inp) if op == dist.ReduceOp.SUM else None
     if nc is not None:
         w = nc.reduce_scatter([out], [inp.contiguous()], "sum", async_op=async_op)

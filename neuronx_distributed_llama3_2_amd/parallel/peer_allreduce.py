@@ -158,3 +158,72 @@ def make_decode_all_reduce(group, nmax: int, device: Optional[torch.device] = No
 
             get_logger().warning("peer all-reduce unavailable (%s); decode all-reduces go through the process group", e)
     return ProcessGroupAllReduce(group)
+
+
+class _PeerWork:
+    """Async handle of a peer collective launched on the group's comm stream: wait() orders the
+    current stream after it; the tensors stay referenced until then."""
+
+    def __init__(self, event, keep):
+        self.event, self.keep = event, keep
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+        self.keep = None
+        return True
+
+    def is_completed(self):
+        return self.event.query()
+
+
+class PeerCollectives:
+    """Sequence-parallel all-gather / reduce-scatter over the peer region (csrc/peer_allreduce.hip
+    peer_coll_kernel): every rank publishes its input once and reads each peer's slot directly, so a
+    node's 7 xGMI links all carry the gather at once, where a ring moves one hop per link
+    step.  All calls of a group run on ONE comm stream (the host issue order, identical on every rank,
+    is the execution order the epoch protocol relies on).  The region grows collectively -- every rank
+    meets the same-sized first call at the same point -- after a device sync and a group barrier.
+    Opt-in (NXD_SP_PEER=1, parallel/comm.py): measured on ranks sharing one GPU only."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.par = None
+        self.cap = 0
+        self.stream = None
+
+    def _ensure(self, nbytes: int) -> PeerAllReduce:
+        if self.par is None or nbytes > self.cap:
+            cap = max(1 << 20, 1 << (int(nbytes) - 1).bit_length())
+            if self.par is not None:
+                torch.cuda.synchronize()
+                dist.barrier(group=self.group)
+                self.par.close()
+            self.par = PeerAllReduce(self.group, nmax=cap // 4)
+            self.cap = cap
+            if self.stream is None:
+                self.stream = torch.cuda.Stream(priority=-1)
+        return self.par
+
+    def _launch(self, inp, out, mode, nbytes, async_op):
+        par = self._ensure(nbytes)
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            par.C.peer_coll(par.h, inp, out, mode)
+        if async_op:
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            return _PeerWork(ev, (inp, out))
+        cur.wait_stream(self.stream)
+        return None
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        inp = inp.contiguous()
+        return self._launch(inp, out, 0, inp.numel() * inp.element_size(), async_op)
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        inp = inp.contiguous()
+        return self._launch(inp, out, 1, inp.numel() * inp.element_size(), async_op)
+
+    def error_count(self) -> int:
+        return self.par.error_count() if self.par is not None else 0

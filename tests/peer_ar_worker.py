@@ -61,6 +61,30 @@ def main():
         par.gather_(sl[rank].clone(), out)
         assert torch.equal(out, torch.cat(sl, dim=1)), it
         checks += 1
+    # sequence-parallel all-gather / reduce-scatter (PeerCollectives: its own region, comm stream,
+    # async handles, region growth)
+    from neuronx_distributed_llama3_2_amd.parallel.peer_allreduce import PeerCollectives
+
+    pc = PeerCollectives(None)
+    for it, (n, dt) in enumerate([(4096, torch.bfloat16), (1 << 19, torch.bfloat16), (8, torch.float32),
+                                  (3 << 16, torch.float32), (1 << 20, torch.bfloat16)]):
+        shards = [partial(700 + it, r, n).to(dt) for r in range(world)]
+        out = torch.empty(world * n, dtype=dt, device="cuda")
+        w = pc.all_gather(out, shards[rank].clone(), async_op=bool(it % 2))
+        if w is not None:
+            w.wait()
+        assert torch.equal(out, torch.cat(shards)), ("ag", it)
+        fulls = [partial(800 + it, r, world * n).to(dt) for r in range(world)]
+        want = torch.zeros(n, device="cuda")
+        for f in fulls:
+            want += f[rank * n:(rank + 1) * n].float()
+        rs = torch.empty(n, dtype=dt, device="cuda")
+        w = pc.reduce_scatter(rs, fulls[rank].clone(), async_op=not bool(it % 2))
+        if w is not None:
+            w.wait()
+        assert torch.equal(rs, want.to(dt)), ("rs", it)
+        checks += 1
+    errs_coll = pc.error_count()
     # inside a hipGraph: 4 calls per replay (an even and an odd count of calls between replays)
     n = 2048
     sin = torch.zeros(4, n, device="cuda")
@@ -102,7 +126,7 @@ def main():
         par.sum_(x, out)
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / 200 * 1e6
-    errs = par.error_count()
+    errs = par.error_count() + errs_coll
     dist.barrier()
     if rank == 0:
         with open(sys.argv[1], "w") as f:

@@ -16,8 +16,8 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(n, *extra, model="tiny"):
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+def _run(n, *extra, model="tiny", env_extra=None):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", **(env_extra or {}))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
     # lr 3e-3: three AdamW steps move the loss away from ln V, so the final loss is a check of the
@@ -49,6 +49,17 @@ def test_bench_tp_sp_ranks_on_one_gpu(n):
     ref = _tp1("tiny8")
     assert rec["value"] > 0 and abs(rec["loss"] - math.log(1024)) > 0.02, rec   # the loss moved
     assert abs(rec["loss"] - ref["loss"]) < 1e-2 * ref["loss"], (rec["loss"], ref["loss"])
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_tp_sp_on_peer_collectives(n):
+    """The sequence-parallel all-gathers / reduce-scatters on the IPC peer kernels (NXD_SP_PEER=1,
+    parallel/peer_allreduce.py PeerCollectives) instead of the process group: same training loss as
+    the process-group run of the same ranks (reduce-scatters summed in fp32 in rank order)."""
+    rec = _run(n, model="tiny8", env_extra={"NXD_SP_PEER": "1"})
+    assert rec["config"]["parallelism"] == f"tp{n}_sp"
+    ref = _run(n, model="tiny8")
+    assert abs(rec["loss"] - ref["loss"]) < 2e-3 * ref["loss"], (rec["loss"], ref["loss"])
 
 
 def test_bench_dp_zero1_ranks_on_one_gpu():

@@ -1,6 +1,7 @@
 """One-shot peer all-reduce (csrc/peer_allreduce.hip, parallel/peer_allreduce.py) with W processes
 sharing the box's GPU through IPC handles: sum / residual-fold / residual-set modes bitwise against a
-rank-order fp32 recomputation, the vocab-parallel gather, inside replayed hipGraphs too, and no peer ever missing its flag."""
+rank-order fp32 recomputation, the vocab-parallel gather, the sequence-parallel all-gather /
+reduce-scatter (async handles, region growth), inside replayed hipGraphs too, and no peer ever missing its flag."""
 import json
 import os
 import socket
@@ -45,4 +46,4 @@ def test_peer_allreduce_ranks_on_one_gpu(world):
     with open(out) as f:
         rec = json.load(f)
     print(rec)
-    assert rec["errors"] == 0 and rec["checks"] == 56
+    assert rec["errors"] == 0 and rec["checks"] == 61
