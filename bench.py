@@ -286,6 +286,8 @@ def supervise_launched_rank(argv) -> int:
         while True:
             c = child.poll()
             if c is not None and c != 0:
+                if rank != 0 and store.check([_PFX + "done"]):
+                    break   # rank 0 already reported this rung's result (a late teardown failure here)
                 rc, why = (c if c > 0 else 128 - c), f"rank {rank} exited {c}"
                 store.set(key + "fail", why)
                 break
