@@ -8,7 +8,8 @@ AdamW, as four runs in fresh processes:
   * the HIP kernels (bf16 copy-out round-to-nearest),
   * the HIP kernels with stochastic rounding of the bf16 weight copy-out,
   * every op on its plain-PyTorch reference (NXD_FORCE_REFERENCE=1) on the same GPU,
-  * TP = 2 + sequence parallel on the HIP kernels, two ranks sharing the GPU over gloo.
+  * TP = 2 + sequence parallel on the HIP kernels, two ranks sharing the GPU (gloo group, SP
+    collectives on the direct-peer IPC kernels).
 Each must agree with the reference run at rtol 0.05 on >= 95 % of the steps after step 100, and the
 loss must end far below ln V (near the chain's 1.13-nat entropy).  The curves are written under
 gpurun_out/convergence/ (copied to profiles/ by hand)."""
@@ -33,7 +34,9 @@ VARIANTS = {
     "hip": ({}, []),
     "hip_sr": ({"NXD_STOCHASTIC_ROUNDING": "1"}, []),
     "reference": ({"NXD_FORCE_REFERENCE": "1"}, []),
-    "tp2_sp_gloo": ({}, ["--tp", "2", "--gloo-gpu"]),
+    # SP all-gathers / reduce-scatters on the peer kernels (host-staged gloo SP collectives made this
+    # variant 240 s of the GPU suite); the remaining collectives (grad norm, CE stats) stay on gloo
+    "tp2_sp_gloo": ({"NXD_SP_PEER": "1"}, ["--tp", "2", "--gloo-gpu"]),
 }
 _curves = {}
 
