@@ -50,6 +50,16 @@ __device__ __forceinline__ u32x4_t pack8(const float* f) {
   return v;
 }
 
+// acc + sum_i a[i] * b[i] over 8 bf16 pairs by 4 v_dot2c_f32_bf16 (products exact in f32, the bf16
+// operands never widened in VGPRs): the decode GEMVs' inner product
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float dot8_bf16(const u32x4_t& a, const u32x4_t& b, float acc) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a[i]), __builtin_bit_cast(bf16x2_t, b[i]), acc, false);
+  return acc;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

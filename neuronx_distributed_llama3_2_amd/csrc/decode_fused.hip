@@ -66,6 +66,7 @@ struct Params {
   // PLAIN only: fp32 output [M, N] (row stride ldy) instead of bf16 y -- a row-parallel projection's
   // partial sum kept unrounded for the tensor-parallel all-reduce (decode at TP > 1)
   float* yf;
+  int dot2;               // inner product on v_dot2c_f32_bf16 (NXD_DECODE_DOT2, default 1)
 };
 
 constexpr int U = 4;   // 512-element k-steps per load round
@@ -291,6 +292,10 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
 #pragma unroll
     for (int r = 0; r < NW; ++r) acc[m][r] = 0.f;
 
+  // inner product: v_dot2c_f32_bf16 on the packed bf16 operands (p.dot2, default), or both operands
+  // widened to f32 and multiplied with FMAs (NXD_DECODE_DOT2=0).  The widening costs one VALU op per
+  // element per activation row: at 8 rows the GEMVs were VALU-bound, 3-4x the single-row time
+  // (gate_up 43.9 vs 12.5 us, profiles/r5k_decode_bs8_kernel_stats.txt)
   auto fma_round = [&](int base, bool first) {
     const bool full = base + 512 * U <= kend;
 #pragma unroll
@@ -300,15 +305,21 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
           if (m < p.M) {
-            float xf[8];
-            if (PREX && first) unpack8(xv0[PREX ? u : 0], xf);
-            else unpack8(*reinterpret_cast<const u32x4_t*>(NORM ? (xs + m * p.K + k) : (p.x + (int64_t)m * p.ldx + k)), xf);
+            const u32x4_t xv = (PREX && first) ? xv0[PREX ? u : 0]
+                                               : *reinterpret_cast<const u32x4_t*>(NORM ? (xs + m * p.K + k) : (p.x + (int64_t)m * p.ldx + k));
+            if (p.dot2) {
 #pragma unroll
-            for (int r = 0; r < NW; ++r) {
-              float wf[8];
-              unpack8(wv[r][u], wf);
+              for (int r = 0; r < NW; ++r) acc[m][r] = dot8_bf16(xv, wv[r][u], acc[m][r]);
+            } else {
+              float xf[8];
+              unpack8(xv, xf);
 #pragma unroll
-              for (int e = 0; e < 8; ++e) acc[m][r] += xf[e] * wf[e];
+              for (int r = 0; r < NW; ++r) {
+                float wf[8];
+                unpack8(wv[r][u], wf);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[m][r] += xf[e] * wf[e];
+              }
             }
           }
         }
@@ -429,6 +440,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
 int g_glu_pairs = 1;   // knob 0: (gate, up) row pairs per wave of the GLU projection (1 | 2)
 int g_ks = 0;          // knob 1: k-slices per row group (0 = pick_ks)
 int g_pf = -1;         // knob 2: early epilogue / prologue reads (Params::pf; NXD_DECODE_EPI_PF, default 1)
+int g_dot2 = -1;       // knob 6: v_dot2c inner product (Params::dot2; NXD_DECODE_DOT2, default 1)
 int g_occ = -1;        // knob 5: bs = 1 two-row kernels at 7 | 8 waves / SIMD (dgemv_kernel_occ; NXD_DECODE_OCC, 0 = natural)
 
 // per-projection override (A/B): NXD_DECODE_KS_PLAIN / _RESID / _GLU / _QKV = 1 | 2 | 4
@@ -515,6 +527,7 @@ void dgemv_set_knob(int which, int value) {
   else if (which == 1) dfused::g_ks = value;
   else if (which == 2) dfused::g_pf = value != 0;
   else if (which == 5) dfused::g_occ = value;
+  else if (which == 6) dfused::g_dot2 = value != 0;
 }
 
 int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,
@@ -540,6 +553,11 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
   p.xrows = xrows;
   p.xcopy = static_cast<uint16_t*>(xcopy);
   p.yf = yf;
+  if (dfused::g_dot2 < 0) {
+    const char* e = getenv("NXD_DECODE_DOT2");
+    dfused::g_dot2 = e ? (atoi(e) != 0) : 1;
+  }
+  p.dot2 = dfused::g_dot2;
   if (dfused::g_occ < 0) {
     const char* e = getenv("NXD_DECODE_OCC");
     dfused::g_occ = e ? atoi(e) : 0;

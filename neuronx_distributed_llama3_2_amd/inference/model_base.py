@@ -44,6 +44,10 @@ _PREFETCH_WGS = int(os.environ.get("NXD_DECODE_PREFETCH_WGS", "256"))
 # from run to run; InferenceConfig(deterministic=True) or NXD_DECODE_ATTN_OPROJ=0 takes the
 # two-launch path (bitwise-reproducible decode, ~5 % slower per token).
 _ATTN_OPROJ = os.environ.get("NXD_DECODE_ATTN_OPROJ", "1") == "1"
+# ... up to this many sequences per step: every (sequence, kv head) workgroup group of the fused
+# launch streams its own copy of the o_proj block, so at batch B it reads Wo B times; above the cap
+# the attention and the o_proj GEMV (one read of Wo for all rows) run as two launches
+_ATTN_OPROJ_MAXB = int(os.environ.get("NXD_DECODE_ATTN_OPROJ_MAXB", "1000000"))
 # The token-embedding gather folded into the first layer's QKV launch (its RMSNorm prologue reads the
 # embedding row of each token id and workgroup 0 writes it to the residual stream): one launch less
 # per decode step.  NXD_DECODE_EMB_FUSED=0 keeps the separate embedding kernel (A/B).
@@ -224,7 +228,8 @@ class DecoderInferenceMixin:
                 # spare workgroups of the attention launch pull o_proj and the head of gate_up into
                 # the Infinity Cache while the (latency-bound) attention leaves HBM idle
                 C.decode_attn_prefetch(attn.o_proj.weight, -1, w_gu, int(_PREFETCH_MB * 2**20), _PREFETCH_WGS)
-            fuse_o = _ATTN_OPROJ and _PREFETCH_MB <= 0 and not getattr(self, "_decode_deterministic", False)
+            fuse_o = (_ATTN_OPROJ and _PREFETCH_MB <= 0 and B <= _ATTN_OPROJ_MAXB
+                      and not getattr(self, "_decode_deterministic", False))
             oacc = self._decode_oacc(M, res) if fuse_o else None
             if oacc is not None and C.decode_attn_oproj(q, kc, vc, sid32, cache_len.to(torch.int32), attn.o_proj.weight,
                                                         oacc, 1.0 / math.sqrt(D)):
@@ -310,7 +315,7 @@ class DecoderInferenceMixin:
         ar.set_residual_(ebuf, res)                                   # res = the embedding rows
         qkv = torch.empty((M, W), dtype=res.dtype, device=res.device)
         clen32 = cache_len.to(torch.int32)
-        fuse_o = _ATTN_OPROJ and not getattr(self, "_decode_deterministic", False)
+        fuse_o = _ATTN_OPROJ and B <= _ATTN_OPROJ_MAXB and not getattr(self, "_decode_deterministic", False)
         for i, layer in enumerate(self.model.layers):
             attn = layer.self_attn
             w_qkv = attn.qkv_proj._fused_weight_bias()[0] if hasattr(attn.qkv_proj, "_fused_weight_bias") \
