@@ -52,11 +52,15 @@ __device__ __forceinline__ u32x4_t pack8(const float* f) {
 
 // acc + sum_i a[i] * b[i] over 8 bf16 pairs by 4 v_dot2c_f32_bf16 (products exact in f32, the bf16
 // operands never widened in VGPRs): the decode GEMVs' inner product
+// (The pairs are taken with __builtin_shufflevector from the bf16x8 view: bit-casting the extracted
+// dword a[i] to bf16x2 made hipcc (ROCm 7.2) feed element 0's registers to all four instructions.)
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float dot8_bf16(const u32x4_t& a, const u32x4_t& b, float acc) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a[i]), __builtin_bit_cast(bf16x2_t, b[i]), acc, false);
+  const bf16x8_t av = __builtin_bit_cast(bf16x8_t, a), bv = __builtin_bit_cast(bf16x8_t, b);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av, av, 0, 1), __builtin_shufflevector(bv, bv, 0, 1), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av, av, 2, 3), __builtin_shufflevector(bv, bv, 2, 3), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av, av, 4, 5), __builtin_shufflevector(bv, bv, 4, 5), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(av, av, 6, 7), __builtin_shufflevector(bv, bv, 6, 7), acc, false);
   return acc;
 }
 

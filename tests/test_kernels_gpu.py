@@ -622,3 +622,30 @@ def test_rmsnorm_rows_path_vs_fp32(H, T):
     assert _rel(mg - mg0, wf.grad) < 1e-3
     for a, b in zip(outs[True], outs[False]):
         assert _rel(a, b) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 2, 4, 8])
+@pytest.mark.parametrize("N,K", [(2048, 2048), (4096, 8192), (1000, 520)])
+@pytest.mark.parametrize("dot2", [0, 1])
+def test_dgemv_plain_matches_fp32(M, N, K, dot2):
+    """Decode GEMV y = x W^T (PLAIN epilogue, with and without the RMSNorm prologue) on both inner
+    products (v_dot2c_f32_bf16 / widened FMAs) against fp32."""
+    C = _ext.ext()
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
+    try:
+        C.decode_set_knob(6, dot2)
+        y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        C.dgemv(0, x, None, 0.0, w, y, 0, 0, 0, None, None, None, 1, None, None, None)
+        ref = x.float() @ w.float().t()
+        assert _rel(y, ref) < 1e-2
+        if M * K > 32768:   # the RMSNorm prologue holds the normalised rows in 64 KiB of LDS
+            return
+        yn = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        C.dgemv(0, x, nw, 1e-5, w, yn, 0, 0, 0, None, None, None, 1, None, None, None)
+        xf = x.float()
+        h = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)).to(torch.bfloat16).float() * nw.float()
+        assert _rel(yn, h.to(torch.bfloat16).float() @ w.float().t()) < 1e-2
+    finally:
+        C.decode_set_knob(6, 1)
