@@ -295,7 +295,7 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
   // inner product: v_dot2c_f32_bf16 on the packed bf16 operands (p.dot2, default), or both operands
   // widened to f32 and multiplied with FMAs (NXD_DECODE_DOT2=0).  The widening costs one VALU op per
   // element per activation row: at 8 rows the GEMVs were VALU-bound, 3-4x the single-row time
-  // (gate_up 43.9 vs 12.5 us, profiles/r5k_decode_bs8_kernel_stats.txt)
+  // (gate_up 43.9 vs 12.5 us, profiles/r5k_decode_bs8_kernel_stats_fma.csv)
   auto fma_round = [&](int base, bool first) {
     const bool full = base + 512 * U <= kend;
 #pragma unroll

@@ -46,8 +46,10 @@ _PREFETCH_WGS = int(os.environ.get("NXD_DECODE_PREFETCH_WGS", "256"))
 _ATTN_OPROJ = os.environ.get("NXD_DECODE_ATTN_OPROJ", "1") == "1"
 # ... up to this many sequences per step: every (sequence, kv head) workgroup group of the fused
 # launch streams its own copy of the o_proj block, so at batch B it reads Wo B times; above the cap
-# the attention and the o_proj GEMV (one read of Wo for all rows) run as two launches
-_ATTN_OPROJ_MAXB = int(os.environ.get("NXD_DECODE_ATTN_OPROJ_MAXB", "1000000"))
+# the attention and the o_proj GEMV (one read of Wo for all rows) run as two launches.  Llama-3.2-1B
+# ms per step fused / two launches: B=2 0.760 / 0.802, B=4 1.096 / 1.083, B=8 1.91 / 1.76
+# (profiles/r5l_decode_dot2_batch_ab.jsonl)
+_ATTN_OPROJ_MAXB = int(os.environ.get("NXD_DECODE_ATTN_OPROJ_MAXB", "2"))
 # The token-embedding gather folded into the first layer's QKV launch (its RMSNorm prologue reads the
 # embedding row of each token id and workgroup 0 writes it to the residual stream): one launch less
 # per decode step.  NXD_DECODE_EMB_FUSED=0 keeps the separate embedding kernel (A/B).
