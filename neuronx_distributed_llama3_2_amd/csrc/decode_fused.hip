@@ -435,6 +435,303 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
 }
 
 
+// ---------------------------------------------------------------------------------------------
+// M = 2..8 activation rows on v_mfma_f32_16x16x32_bf16.  With the VALU inner product every 16-B
+// weight chunk is multiplied by M activation chunks that each wave re-reads (LDS or L2) and the
+// FMAs scale with M: at 8 rows the GEMVs ran 3-4x their single-row time (gate_up 35.7 vs 12.4 us
+// with dot2, profiles/r5k_decode_bs8_kernel_stats_*).  Here a wave owns a tile of 16 weight rows
+// = the 16 columns of the MFMA B operand (lane l loads 16 B of row (l & 15) at k 8 (l >> 4), the
+// same 16-B nontemporal loads as the VALU body), the activations are the A operand (rows >= M
+// zero), and one MFMA consumes 1 KiB of weights: the arithmetic no longer grows with M.
+// Tiles: PLAIN / RESID 16 consecutive rows; GLU 8 gate rows (columns 0-7) + their 8 up rows
+// (8-15); ROPE_KV 8 rotary pairs of one q / k head (d0..d0+7 | the same + D/2) or 16 v rows --
+// the pair partner is 8 lanes away (one xor-8 shuffle in the epilogue).  KS waves split K and
+// reduce through LDS; NWV waves per workgroup (4, or 8 when KS = 8).
+// C layout of the 16x16 MFMA: lane l holds rows m = 4 (l >> 4) + i (i < 4) of column l & 15, so
+// lanes 0-31 carry the <= 8 real rows.
+template <int EPI, bool NORM, int KS, int NWV, bool XI = false>
+__global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* xs = reinterpret_cast<uint16_t*>(smem);   // NORM: [M][K] normalised bf16 rows
+  __shared__ float red[NWV][8];
+  __shared__ f32x4_t part[KS > 1 ? NWV : 1][32];
+  constexpr int G = NWV / KS;
+  constexpr int U = 8;                                 // 32-deep k-steps per load round
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rg = wid / KS, ks = wid % KS;
+  const int tile = blockIdx.x * G + rg;
+  const int c = lane & 15;
+
+  // ---- this lane's weight row (B column c) and the tile's output mapping
+  int row = 0;
+  bool active = true;   // tile-uniform
+  const int half = p.D / 2;
+  const int qk_tiles = EPI == ROPE_KV ? (p.nq + p.nkv) * (half / 8) : 0;
+  if (EPI == GLU) {
+    active = tile * 8 < p.N;
+    const int g = min(tile * 8 + (c & 7), p.N - 1);
+    row = c < 8 ? g : g + p.N;
+  } else if (EPI == ROPE_KV) {
+    if (tile < qk_tiles) {
+      const int h = tile / (half / 8), d0 = (tile % (half / 8)) * 8;
+      row = h * p.D + d0 + (c & 7) + (c < 8 ? 0 : half);
+    } else {
+      const int v0 = (p.nq + p.nkv) * p.D + (tile - qk_tiles) * 16;
+      active = (tile - qk_tiles) * 16 < p.nkv * p.D;
+      row = min(v0 + c, p.N - 1);
+    }
+  } else {
+    active = tile * 16 < p.N;
+    row = min(tile * 16 + c, p.N - 1);
+  }
+  const uint16_t* wrow = p.w + (int64_t)row * p.ldw;
+
+  // ---- k range of this slice (32-aligned), first weight round issued before the prologue
+  const int kc = ((p.K + KS - 1) / KS + 31) & ~31;
+  const int kbeg = min(ks * kc, p.K), kend = min(p.K, kbeg + kc);
+  const int kq = 8 * (lane >> 4);                      // this lane's k offset inside a 32-step
+  u32x4_t wv[U];
+  auto load_round = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = min(base + 32 * u + kq, kend - 8);
+      wv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(wrow + k));
+    }
+  };
+  if (kbeg < kend) load_round(kbeg);
+
+  auto xrow = [&](int m) -> const uint16_t* {
+    if constexpr (XI) {
+      const int64_t t = p.xidx[m];
+      return p.x + (t < 0 ? 0 : (t >= p.xrows ? p.xrows - 1 : t)) * p.ldx;
+    } else {
+      return p.x + (int64_t)m * p.ldx;
+    }
+  };
+  auto xok = [&](int m) -> bool {
+    if constexpr (XI) {
+      const int64_t t = p.xidx[m];
+      return t >= 0 && t < p.xrows;
+    } else {
+      return true;
+    }
+  };
+
+  // ---- RMSNorm prologue (as the VALU body): rows -> LDS, x += bf16(xadd), normalised in place
+  if constexpr (NORM) {
+    constexpr int NT = 64 * NWV;
+    float ss[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) ss[m] = 0.f;
+    for (int k = tid * 8; k < p.K; k += NT * 8) {
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        if (m < p.M) {
+          u32x4_t v = *reinterpret_cast<const u32x4_t*>(xrow(m) + k);
+          if (XI && !xok(m)) v = u32x4_t{0u, 0u, 0u, 0u};
+          float f[8];
+          unpack8(v, f);
+          if (p.xadd) {
+            const f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k);
+            const f32x4_t a1 = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)m * p.K + k + 4);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = bf2f(f2bf(f[j] + bf2f(f2bf(j < 4 ? a0[j] : a1[j - 4]))));
+            v = pack8(f);
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss[m] += f[j] * f[j];
+          *reinterpret_cast<u32x4_t*>(xs + m * p.K + k) = v;
+          if (XI && blockIdx.x == 0 && p.xcopy) *reinterpret_cast<u32x4_t*>(p.xcopy + (int64_t)m * p.K + k) = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const float sm = wave_sum(ss[m]);
+      if (lane == 0) red[wid][m] = sm;
+    }
+    __syncthreads();
+    float rstd[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) t += red[w][m];
+      rstd[m] = rsqrtf(t / (float)p.K + p.eps);
+    }
+    for (int k = tid * 8; k < p.K; k += NT * 8) {
+      float g[8];
+      unpack8(*reinterpret_cast<const u32x4_t*>(p.norm_w + k), g);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        if (m < p.M) {
+          float f[8];
+          unpack8(*reinterpret_cast<const u32x4_t*>(xs + m * p.K + k), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = f[j] * rstd[m] * g[j];
+          *reinterpret_cast<u32x4_t*>(xs + m * p.K + k) = pack8(f);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- main loop: A = activation rows (lane row c < M, k 8 (l >> 4)), B = the weight tile
+  const bool arow = c < p.M;
+  // activation rows >= M and k >= kend read an in-bounds chunk that is replaced by zeros (an
+  // unpredicated load; a predicated one made hipcc spill the whole round)
+  const uint16_t* xr = NORM ? xs + min(c, p.M - 1) * p.K : p.x + (int64_t)min(c, p.M - 1) * p.ldx;
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int base = kbeg; base < kend; base += 32 * U) {
+    if (base != kbeg) load_round(base);
+    u32x4_t xa[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = base + 32 * u + kq;
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(xr + min(k, kend - 8));
+      xa[u] = (arow && k < kend) ? v : u32x4_t{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (base + 32 * u < kend)   // wave-uniform
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, xa[u]), __builtin_bit_cast(bf16x8_t, wv[u]), acc, 0, 0, 0);
+    }
+  }
+
+  // ---- k-slice reduction (lanes 0-31 hold the real rows)
+  if constexpr (KS > 1) {
+    if (lane < 32) part[wid][lane] = acc;
+    __syncthreads();
+    if (ks != 0) return;
+#pragma unroll
+    for (int j = 1; j < KS; ++j) {
+      const f32x4_t o = part[wid + j][lane & 31];
+      acc += o;
+    }
+  }
+  if (!active) return;
+
+  // ---- epilogue: lane (c, rows 4 (lane >> 4) + i)
+  const int m0 = 4 * (lane >> 4);
+  if (EPI == GLU) {
+    f32x4_t up;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(acc[i], 8, 64);
+    const int n = tile * 8 + c;
+    if (lane >= 32 || c >= 8 || n >= p.N) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + i;
+      if (m < p.M) {
+        const float g = acc[i];
+        p.y[(int64_t)m * p.ldy + n] = f2bf(g / (1.f + __expf(-g)) * up[i]);
+      }
+    }
+    return;
+  }
+  if (EPI == ROPE_KV) {
+    const int qk_rows = (p.nq + p.nkv) * p.D;
+    f32x4_t other;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) other[i] = __shfl_xor(acc[i], 8, 64);
+    if (lane >= 32) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + i;
+      if (m >= p.M) continue;
+      const int64_t ps = p.pos[m];
+      const int b = m / p.T;
+      const int cb = p.cache_idx ? p.cache_idx[b] : b;
+      const bool in_cache = ps >= 0 && ps < p.Lmax;
+      uint16_t* yr = p.y + (int64_t)m * p.ldy;
+      if (tile < qk_tiles) {
+        const int h = row / p.D, d = (row % p.D) % half;
+        const int64_t pt = ps < 0 ? 0 : (ps >= p.max_pos ? p.max_pos - 1 : ps);
+        const float cs = p.cos_t[pt * half + d], sn = p.sin_t[pt * half + d];
+        const float mine = bf2f(f2bf(acc[i])), part2 = bf2f(f2bf(other[i]));   // bf16 projection outputs
+        const uint16_t o = c < 8 ? f2bf(mine * cs - part2 * sn) : f2bf(mine * cs + part2 * sn);
+        yr[row] = o;
+        if (h >= p.nq && in_cache)
+          p.kc[(int64_t)cb * p.c_sb + (int64_t)(h - p.nq) * p.c_sh + ps * p.c_sl + (row % p.D)] = o;
+      } else {
+        const int r = (p.nq + p.nkv) * p.D + (tile - qk_tiles) * 16 + c;
+        if (r >= p.N) continue;
+        const uint16_t o = f2bf(acc[i]);
+        yr[r] = o;
+        const int vr = r - qk_rows;
+        if (in_cache) p.vc[(int64_t)cb * p.c_sb + (int64_t)(vr / p.D) * p.c_sh + ps * p.c_sl + vr % p.D] = o;
+      }
+    }
+    return;
+  }
+  const int n = tile * 16 + c;
+  if (lane >= 32 || n >= p.N) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + i;
+    if (m >= p.M) continue;
+    uint16_t* yr = p.y + (int64_t)m * p.ldy;
+    if (EPI == RESID) {
+      float yv = bf2f(yr[n]);
+      if (p.yadd) {
+        float* ya = p.yadd + (int64_t)m * p.N + n;
+        yv = bf2f(f2bf(yv + bf2f(f2bf(*ya))));
+        *ya = 0.f;
+      }
+      yr[n] = f2bf(yv + bf2f(f2bf(acc[i])));
+    } else if (p.yf) {
+      p.yf[(int64_t)m * p.ldy + n] = acc[i];
+    } else {
+      yr[n] = f2bf(acc[i]);
+    }
+  }
+}
+
+int g_mfma = -1;   // knob 7: M >= 2 rows on dmm_kernel (NXD_DECODE_MFMA, default 1)
+
+template <int EPI, bool NORM, bool XI>
+static int launch_mfma(const Params& p, int tiles, hipStream_t s) {
+  // k-slices: fill ~2,048 waves while a slice keeps >= 256 elements (qkv / o_proj / down -> 8,
+  // gate_up -> 2, lm_head -> 1)
+  int ks = 1;
+  while (ks < 8 && (int64_t)tiles * ks < 2048 && p.K / (ks * 2) >= 256) ks *= 2;
+  const size_t lds = NORM ? (size_t)p.M * p.K * 2 : 0;
+#define NXD_DMM(KSV, NW)                                                                              \
+  hipLaunchKernelGGL((dmm_kernel<EPI, NORM, KSV, NW, XI>), dim3((unsigned)((tiles + (NW / KSV) - 1) / (NW / KSV))), \
+                     dim3(64 * NW), lds, s, p)
+  if (ks == 8) NXD_DMM(8, 8);
+  else if (ks == 4) NXD_DMM(4, 4);
+  else if (ks == 2) NXD_DMM(2, 4);
+  else NXD_DMM(1, 4);
+#undef NXD_DMM
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+static int dispatch_mfma(const Params& p, int epi, bool norm, hipStream_t s) {
+  switch (epi) {
+    case PLAIN: {
+      const int tiles = (p.N + 15) / 16;
+      return norm ? launch_mfma<PLAIN, true, false>(p, tiles, s) : launch_mfma<PLAIN, false, false>(p, tiles, s);
+    }
+    case RESID: {
+      const int tiles = (p.N + 15) / 16;
+      return norm ? launch_mfma<RESID, true, false>(p, tiles, s) : launch_mfma<RESID, false, false>(p, tiles, s);
+    }
+    case GLU: {
+      const int tiles = (p.N + 7) / 8;
+      return norm ? launch_mfma<GLU, true, false>(p, tiles, s) : launch_mfma<GLU, false, false>(p, tiles, s);
+    }
+    case ROPE_KV: {
+      const int tiles = (p.nq + p.nkv) * (p.D / 2 / 8) + (p.nkv * p.D + 15) / 16;
+      if (p.xidx) return norm ? launch_mfma<ROPE_KV, true, true>(p, tiles, s) : -4;
+      return norm ? launch_mfma<ROPE_KV, true, false>(p, tiles, s) : launch_mfma<ROPE_KV, false, false>(p, tiles, s);
+    }
+  }
+  return -1;
+}
+
+
 // k-slices per row group: split K while the grid stays <= 8192 waves and slices keep >= 1024
 // elements (o_proj 2048 x 2048 -> 2, down 2048 x 8192 -> 4, gate_up / lm_head / QKV -> 1)
 int g_glu_pairs = 1;   // knob 0: (gate, up) row pairs per wave of the GLU projection (1 | 2)
@@ -528,6 +825,7 @@ void dgemv_set_knob(int which, int value) {
   else if (which == 2) dfused::g_pf = value != 0;
   else if (which == 5) dfused::g_occ = value;
   else if (which == 6) dfused::g_dot2 = value != 0;
+  else if (which == 7) dfused::g_mfma = value != 0;
 }
 
 int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,
@@ -565,6 +863,13 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
     if (gp && atoi(gp) == 2) dfused::g_glu_pairs = 2;
   }
   const bool norm = norm_w != nullptr;
+  if (dfused::g_mfma < 0) {
+    const char* e = getenv("NXD_DECODE_MFMA");
+    dfused::g_mfma = e ? (atoi(e) != 0) : 1;
+  }
+  // MFMA rows need whole rotary 8-pair tiles (D / 2 % 8 == 0) and 16-B aligned 32-deep k-steps
+  if (M >= 2 && dfused::g_mfma && (epi != dfused::ROPE_KV || (D / 2) % 8 == 0))
+    return dfused::dispatch_mfma(p, epi, norm, stream);
   if (M == 1) return dfused::dispatch<1>(p, epi, norm, stream);
   if (M == 2) return dfused::dispatch<2>(p, epi, norm, stream);
   if (M <= 4) return dfused::dispatch<4>(p, epi, norm, stream);
