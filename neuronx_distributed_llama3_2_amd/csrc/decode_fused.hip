@@ -688,19 +688,21 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   }
 }
 
-int g_mfma = -1;   // knob 7: M >= 2 rows on dmm_kernel (NXD_DECODE_MFMA, default 1)
+int g_mfma = -1;   // knob 7: dmm_kernel from this many activation rows on (NXD_DECODE_MFMA; 0 = never)
 
 template <int EPI, bool NORM, bool XI>
 static int launch_mfma(const Params& p, int tiles, hipStream_t s) {
-  // k-slices: fill ~2,048 waves while a slice keeps >= 256 elements (qkv / o_proj / down -> 8,
-  // gate_up -> 2, lm_head -> 1)
+  // k-slices: fill ~8,192 waves (one weight round of 8 KiB each in flight: a CU needs ~100 KiB
+  // outstanding to stream) while a slice keeps >= 256 elements: gate_up / qkv / o_proj -> 8,
+  // down -> 16, lm_head -> 2 at Llama-3.2-1B
   int ks = 1;
-  while (ks < 8 && (int64_t)tiles * ks < 2048 && p.K / (ks * 2) >= 256) ks *= 2;
+  while (ks < 16 && (int64_t)tiles * ks < 8192 && p.K / (ks * 2) >= 256) ks *= 2;
   const size_t lds = NORM ? (size_t)p.M * p.K * 2 : 0;
 #define NXD_DMM(KSV, NW)                                                                              \
   hipLaunchKernelGGL((dmm_kernel<EPI, NORM, KSV, NW, XI>), dim3((unsigned)((tiles + (NW / KSV) - 1) / (NW / KSV))), \
                      dim3(64 * NW), lds, s, p)
-  if (ks == 8) NXD_DMM(8, 8);
+  if (ks == 16) NXD_DMM(16, 16);
+  else if (ks == 8) NXD_DMM(8, 8);
   else if (ks == 4) NXD_DMM(4, 4);
   else if (ks == 2) NXD_DMM(2, 4);
   else NXD_DMM(1, 4);
@@ -825,7 +827,7 @@ void dgemv_set_knob(int which, int value) {
   else if (which == 2) dfused::g_pf = value != 0;
   else if (which == 5) dfused::g_occ = value;
   else if (which == 6) dfused::g_dot2 = value != 0;
-  else if (which == 7) dfused::g_mfma = value != 0;
+  else if (which == 7) dfused::g_mfma = value;
 }
 
 int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,
@@ -865,10 +867,10 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
   const bool norm = norm_w != nullptr;
   if (dfused::g_mfma < 0) {
     const char* e = getenv("NXD_DECODE_MFMA");
-    dfused::g_mfma = e ? (atoi(e) != 0) : 1;
+    dfused::g_mfma = e ? atoi(e) : 2;
   }
   // MFMA rows need whole rotary 8-pair tiles (D / 2 % 8 == 0) and 16-B aligned 32-deep k-steps
-  if (M >= 2 && dfused::g_mfma && (epi != dfused::ROPE_KV || (D / 2) % 8 == 0))
+  if (M >= 2 && dfused::g_mfma > 0 && M >= dfused::g_mfma && (epi != dfused::ROPE_KV || (D / 2) % 8 == 0))
     return dfused::dispatch_mfma(p, epi, norm, stream);
   if (M == 1) return dfused::dispatch<1>(p, epi, norm, stream);
   if (M == 2) return dfused::dispatch<2>(p, epi, norm, stream);

@@ -626,11 +626,13 @@ def test_rmsnorm_rows_path_vs_fp32(H, T):
 
 @pytest.mark.parametrize("M", [1, 2, 4, 8])
 @pytest.mark.parametrize("N,K", [(2048, 2048), (4096, 8192), (1000, 520)])
-@pytest.mark.parametrize("dot2", [0, 1])
-def test_dgemv_plain_matches_fp32(M, N, K, dot2):
-    """Decode GEMV y = x W^T (PLAIN epilogue, with and without the RMSNorm prologue) on both inner
-    products (v_dot2c_f32_bf16 / widened FMAs) against fp32."""
+@pytest.mark.parametrize("path", ["fma", "dot2", "mfma"])
+def test_dgemv_plain_matches_fp32(M, N, K, path):
+    """Decode GEMV y = x W^T (PLAIN epilogue, with and without the RMSNorm prologue) on every body:
+    VALU with widened FMAs / v_dot2c_f32_bf16, and the MFMA tiles of 2-8 rows, against fp32."""
     C = _ext.ext()
+    C.decode_set_knob(7, 2 if path == "mfma" else 0)
+    dot2 = 0 if path == "fma" else 1
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
     nw = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
@@ -649,3 +651,4 @@ def test_dgemv_plain_matches_fp32(M, N, K, dot2):
         assert _rel(yn, h.to(torch.bfloat16).float() @ w.float().t()) < 1e-2
     finally:
         C.decode_set_knob(6, 1)
+        C.decode_set_knob(7, 2)
