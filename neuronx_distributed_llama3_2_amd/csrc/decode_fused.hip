@@ -692,11 +692,15 @@ int g_mfma = -1;   // knob 7: dmm_kernel from this many activation rows on (NXD_
 
 template <int EPI, bool NORM, bool XI>
 static int launch_mfma(const Params& p, int tiles, hipStream_t s) {
-  // k-slices: fill ~8,192 waves (one weight round of 8 KiB each in flight: a CU needs ~100 KiB
-  // outstanding to stream) while a slice keeps >= 256 elements: gate_up / qkv / o_proj -> 8,
-  // down -> 16, lm_head -> 2 at Llama-3.2-1B
+  // k-slices: fill NXD_DECODE_MFMA_WAVES (default 2,048) waves while a slice keeps >= 256 elements
+  // (Llama-3.2-1B at 2,048: qkv / o_proj / down -> 8, gate_up -> 2, lm_head -> 1)
+  static const int target = [] {
+    const char* e = getenv("NXD_DECODE_MFMA_WAVES");
+    const int v = e ? atoi(e) : 2048;
+    return v > 0 ? v : 2048;
+  }();
   int ks = 1;
-  while (ks < 16 && (int64_t)tiles * ks < 8192 && p.K / (ks * 2) >= 256) ks *= 2;
+  while (ks < 16 && (int64_t)tiles * ks < target && p.K / (ks * 2) >= 256) ks *= 2;
   const size_t lds = NORM ? (size_t)p.M * p.K * 2 : 0;
 #define NXD_DMM(KSV, NW)                                                                              \
   hipLaunchKernelGGL((dmm_kernel<EPI, NORM, KSV, NW, XI>), dim3((unsigned)((tiles + (NW / KSV) - 1) / (NW / KSV))), \
