@@ -486,7 +486,7 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   }
   const uint16_t* wrow = p.w + (int64_t)row * p.ldw;
 
-  // ---- k range of this slice (32-aligned), first weight round issued before the prologue
+  // ---- k range of this slice (32-aligned); the first weight round goes out before the prologue
   const int kc = ((p.K + KS - 1) / KS + 31) & ~31;
   const int kbeg = min(ks * kc, p.K), kend = min(p.K, kbeg + kc);
   const int kq = 8 * (lane >> 4);                      // this lane's k offset inside a 32-step
@@ -498,8 +498,6 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
       wv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(wrow + k));
     }
   };
-  if (kbeg < kend) load_round(kbeg);
-
   auto xrow = [&](int m) -> const uint16_t* {
     if constexpr (XI) {
       const int64_t t = p.xidx[m];
@@ -516,6 +514,42 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
       return true;
     }
   };
+  // RMSNorm rows of one chunk per thread (K <= 8 x threads): loaded BEFORE the weight round.  vmcnt
+  // retires in issue order, so prologue loads issued after the weights wait for all of them and
+  // the normalisation only starts once the weights have landed (the VALU body's MM = 1 PRE path)
+  constexpr int NTH = 64 * NWV;
+  const bool pre = NORM && p.K <= NTH * 8;
+  u32x4_t xpre[8];
+  if (NORM && pre) {
+    const int k = min(tid * 8, p.K - 8);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) xpre[m] = *reinterpret_cast<const u32x4_t*>(xrow(min(m, p.M - 1)) + k);
+  }
+  if (kbeg < kend) load_round(kbeg);
+  // epilogue operands (residual row + pending fp32 sum; rotary position + cos / sin) issued now,
+  // so they land behind the first weight round instead of as round trips after the reduction
+  const int m0 = 4 * (lane >> 4);
+  uint16_t y_pre[4];
+  float ya_pre[4], cs_pre[4], sn_pre[4];
+  if (EPI == RESID && active && lane < 32 && ks == 0) {
+    const int n = min(tile * 16 + c, p.N - 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = min(m0 + i, p.M - 1);
+      y_pre[i] = p.y[(int64_t)m * p.ldy + n];
+      ya_pre[i] = p.yadd ? p.yadd[(int64_t)m * p.N + n] : 0.f;
+    }
+  }
+  if (EPI == ROPE_KV && active && lane < 32 && ks == 0 && tile < qk_tiles) {
+    const int d = (row % p.D) % half;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t ps = p.pos[min(m0 + i, p.M - 1)];
+      const int64_t pt = ps < 0 ? 0 : (ps >= p.max_pos ? p.max_pos - 1 : ps);
+      cs_pre[i] = p.cos_t[pt * half + d];
+      sn_pre[i] = p.sin_t[pt * half + d];
+    }
+  }
 
   // ---- RMSNorm prologue (as the VALU body): rows -> LDS, x += bf16(xadd), normalised in place
   if constexpr (NORM) {
@@ -527,7 +561,7 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         if (m < p.M) {
-          u32x4_t v = *reinterpret_cast<const u32x4_t*>(xrow(m) + k);
+          u32x4_t v = pre ? xpre[m] : *reinterpret_cast<const u32x4_t*>(xrow(m) + k);
           if (XI && !xok(m)) v = u32x4_t{0u, 0u, 0u, 0u};
           float f[8];
           unpack8(v, f);
@@ -613,7 +647,6 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   if (!active) return;
 
   // ---- epilogue: lane (c, rows 4 (lane >> 4) + i)
-  const int m0 = 4 * (lane >> 4);
   if (EPI == GLU) {
     f32x4_t up;
 #pragma unroll
@@ -646,9 +679,8 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
       const bool in_cache = ps >= 0 && ps < p.Lmax;
       uint16_t* yr = p.y + (int64_t)m * p.ldy;
       if (tile < qk_tiles) {
-        const int h = row / p.D, d = (row % p.D) % half;
-        const int64_t pt = ps < 0 ? 0 : (ps >= p.max_pos ? p.max_pos - 1 : ps);
-        const float cs = p.cos_t[pt * half + d], sn = p.sin_t[pt * half + d];
+        const int h = row / p.D;
+        const float cs = cs_pre[i], sn = sn_pre[i];
         const float mine = bf2f(f2bf(acc[i])), part2 = bf2f(f2bf(other[i]));   // bf16 projection outputs
         const uint16_t o = c < 8 ? f2bf(mine * cs - part2 * sn) : f2bf(mine * cs + part2 * sn);
         yr[row] = o;
@@ -673,11 +705,10 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
     if (m >= p.M) continue;
     uint16_t* yr = p.y + (int64_t)m * p.ldy;
     if (EPI == RESID) {
-      float yv = bf2f(yr[n]);
+      float yv = bf2f(y_pre[i]);
       if (p.yadd) {
-        float* ya = p.yadd + (int64_t)m * p.N + n;
-        yv = bf2f(f2bf(yv + bf2f(f2bf(*ya))));
-        *ya = 0.f;
+        yv = bf2f(f2bf(yv + bf2f(f2bf(ya_pre[i]))));
+        p.yadd[(int64_t)m * p.N + n] = 0.f;
       }
       yr[n] = f2bf(yv + bf2f(f2bf(acc[i])));
     } else if (p.yf) {
