@@ -67,6 +67,7 @@ struct Params {
   // partial sum kept unrounded for the tensor-parallel all-reduce (decode at TP > 1)
   float* yf;
   int dot2;               // inner product on v_dot2c_f32_bf16 (NXD_DECODE_DOT2, default 1)
+  int split;              // dmm_kernel: workgroups per weight tile along K (partials summed in g_sk)
 };
 
 constexpr int U = 4;   // 512-element k-steps per load round
@@ -449,6 +450,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
 // reduce through LDS; NWV waves per workgroup (4, or 8 when KS = 8).
 // C layout of the 16x16 MFMA: lane l holds rows m = 4 (l >> 4) + i (i < 4) of column l & 15, so
 // lanes 0-31 carry the <= 8 real rows.
+constexpr int kSkTiles = 4096;   // weight tiles a split launch may have
+__device__ float g_sk[kSkTiles * 128];   // zero-initialised; every split launch leaves it zero
+__device__ int g_skc[kSkTiles];
+
 template <int EPI, bool NORM, int KS, int NWV, bool XI = false>
 __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -459,7 +464,8 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   constexpr int U = 8;                                 // 32-deep k-steps per load round
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int rg = wid / KS, ks = wid % KS;
-  const int tile = blockIdx.x * G + rg;
+  const int spi = (int)blockIdx.x % p.split;            // this workgroup's K part of its tiles
+  const int tile = ((int)blockIdx.x / p.split) * G + rg;
   const int c = lane & 15;
 
   // ---- this lane's weight row (B column c) and the tile's output mapping
@@ -487,8 +493,9 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   const uint16_t* wrow = p.w + (int64_t)row * p.ldw;
 
   // ---- k range of this slice (32-aligned); the first weight round goes out before the prologue
-  const int kc = ((p.K + KS - 1) / KS + 31) & ~31;
-  const int kbeg = min(ks * kc, p.K), kend = min(p.K, kbeg + kc);
+  const int nparts = p.split * KS;
+  const int kc = ((p.K + nparts - 1) / nparts + 31) & ~31;
+  const int kbeg = min((spi * KS + ks) * kc, p.K), kend = min(p.K, kbeg + kc);
   const int kq = 8 * (lane >> 4);                      // this lane's k offset inside a 32-step
   u32x4_t wv[U];
   auto load_round = [&](int base) {
@@ -646,6 +653,32 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   }
   if (!active) return;
 
+  // ---- split-K across workgroups: every part adds its 16 x 8 partial into the tile's fp32 slot
+  // (float atomics, memory side), takes a ticket, and the last part reads the sum back, re-zeroes
+  // the slot and counter for the next launch, and runs the epilogue.  No workgroup waits on another.
+  if (p.split > 1) {
+    float* sk = g_sk + (int64_t)tile * 128;            // [4][32 lanes]: 128 contiguous bytes per add
+    if (lane < 32) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) unsafeAtomicAdd(sk + 32 * i + lane, acc[i]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(g_skc + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    t = __shfl(t, 0, 64);
+    if (t != p.split - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (lane < 32) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i] = __hip_atomic_load(sk + 32 * i + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sk + 32 * i + lane, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (lane == 0) __hip_atomic_store(g_skc + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+
   // ---- epilogue: lane (c, rows 4 (lane >> 4) + i)
   if (EPI == GLU) {
     f32x4_t up;
@@ -722,26 +755,29 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
 int g_mfma = -1;   // knob 7: dmm_kernel from this many activation rows on (NXD_DECODE_MFMA; 0 = never)
 
 template <int EPI, bool NORM, bool XI>
-static int launch_mfma(const Params& p, int tiles, hipStream_t s) {
-  // k-slices: fill NXD_DECODE_MFMA_WAVES (default 2,048) waves while a slice keeps >= 256 elements
-  // (Llama-3.2-1B at 2,048: qkv / o_proj / down -> 8, gate_up -> 2, lm_head -> 1)
+static int launch_mfma(Params p, int tiles, hipStream_t s) {
+  // 4-wave workgroups; K split over KS waves (reduced in LDS) and then over `split` workgroups
+  // (reduced through g_sk) until ~NXD_DECODE_MFMA_WGS (512) workgroups stream while every wave
+  // keeps >= 256 elements of K: Llama-3.2-1B qkv 4 x 2 (384 WGs), o_proj 4 x 2, down 4 x 4 (512),
+  // gate_up 2 x 1 (512), lm_head 1 x 1 (2,004).  One stream at a time uses g_sk (decode is serial).
   static const int target = [] {
-    const char* e = getenv("NXD_DECODE_MFMA_WAVES");
-    const int v = e ? atoi(e) : 2048;
-    return v > 0 ? v : 2048;
+    const char* e = getenv("NXD_DECODE_MFMA_WGS");
+    const int v = e ? atoi(e) : 512;
+    return v > 0 ? v : 512;
   }();
-  int ks = 1;
-  while (ks < 16 && (int64_t)tiles * ks < target && p.K / (ks * 2) >= 256) ks *= 2;
+  int ks = 1, split = 1;
+  auto wgs = [&] { return (int64_t)((tiles + (4 / ks) - 1) / (4 / ks)) * split; };
+  while (wgs() < target && (int64_t)ks * split * 2 * 256 <= p.K) {
+    if (ks < 4) ks *= 2;
+    else split *= 2;
+  }
+  if (tiles > kSkTiles) split = 1;
+  p.split = split;
   const size_t lds = NORM ? (size_t)p.M * p.K * 2 : 0;
-#define NXD_DMM(KSV, NW)                                                                              \
-  hipLaunchKernelGGL((dmm_kernel<EPI, NORM, KSV, NW, XI>), dim3((unsigned)((tiles + (NW / KSV) - 1) / (NW / KSV))), \
-                     dim3(64 * NW), lds, s, p)
-  if (ks == 16) NXD_DMM(16, 16);
-  else if (ks == 8) NXD_DMM(8, 8);
-  else if (ks == 4) NXD_DMM(4, 4);
-  else if (ks == 2) NXD_DMM(2, 4);
-  else NXD_DMM(1, 4);
-#undef NXD_DMM
+  const unsigned grid = (unsigned)wgs();
+  if (ks == 4) hipLaunchKernelGGL((dmm_kernel<EPI, NORM, 4, 4, XI>), dim3(grid), dim3(256), lds, s, p);
+  else if (ks == 2) hipLaunchKernelGGL((dmm_kernel<EPI, NORM, 2, 4, XI>), dim3(grid), dim3(256), lds, s, p);
+  else hipLaunchKernelGGL((dmm_kernel<EPI, NORM, 1, 4, XI>), dim3(grid), dim3(256), lds, s, p);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
