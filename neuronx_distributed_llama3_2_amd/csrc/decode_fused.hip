@@ -450,9 +450,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
 // reduce through LDS; NWV waves per workgroup (4, or 8 when KS = 8).
 // C layout of the 16x16 MFMA: lane l holds rows m = 4 (l >> 4) + i (i < 4) of column l & 15, so
 // lanes 0-31 carry the <= 8 real rows.
-constexpr int kSkTiles = 4096;   // weight tiles a split launch may have
-__device__ float g_sk[kSkTiles * 128];   // zero-initialised; every split launch leaves it zero
-__device__ int g_skc[kSkTiles];
+constexpr int kSkTiles = 1024;   // weight tiles a split launch may have
+constexpr int kMaxSplit = 8;     // workgroups per tile
+__device__ float g_sk[kSkTiles * kMaxSplit * 128];   // per-part partial slots (overwritten every launch)
+__device__ int g_skc[kSkTiles];                      // arrival tickets: zero-initialised, left zero
 
 template <int EPI, bool NORM, int KS, int NWV, bool XI = false>
 __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
@@ -653,14 +654,15 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   }
   if (!active) return;
 
-  // ---- split-K across workgroups: every part adds its 16 x 8 partial into the tile's fp32 slot
-  // (float atomics, memory side), takes a ticket, and the last part reads the sum back, re-zeroes
-  // the slot and counter for the next launch, and runs the epilogue.  No workgroup waits on another.
+  // ---- split-K across workgroups: every part stores its 16 x 8 partial into its own slot, publishes
+  // it (release) and takes a ticket; the last part sums the slots in part order (the same bits
+  // whichever part arrives last), resets the ticket for the next launch, and runs the epilogue.
+  // No workgroup waits on another.
   if (p.split > 1) {
-    float* sk = g_sk + (int64_t)tile * 128;            // [4][32 lanes]: 128 contiguous bytes per add
+    float* sk = g_sk + (int64_t)tile * (kMaxSplit * 128);   // [part][4][32 lanes]
     if (lane < 32) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) unsafeAtomicAdd(sk + 32 * i + lane, acc[i]);
+      for (int i = 0; i < 4; ++i) sk[spi * 128 + 32 * i + lane] = acc[i];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -672,8 +674,9 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
     if (lane < 32) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        acc[i] = __hip_atomic_load(sk + 32 * i + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(sk + 32 * i + lane, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        float v = 0.f;
+        for (int j = 0; j < p.split; ++j) v += sk[j * 128 + 32 * i + lane];
+        acc[i] = v;
       }
     }
     if (lane == 0) __hip_atomic_store(g_skc + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -757,7 +760,7 @@ int g_mfma = -1;   // knob 7: dmm_kernel from this many activation rows on (NXD_
 template <int EPI, bool NORM, bool XI>
 static int launch_mfma(Params p, int tiles, hipStream_t s) {
   // 4-wave workgroups; K split over KS waves (reduced in LDS) and then over `split` workgroups
-  // (reduced through g_sk) until ~NXD_DECODE_MFMA_WGS (512) workgroups stream while every wave
+  // (summed in order through g_sk) until ~NXD_DECODE_MFMA_WGS (512) workgroups stream while every wave
   // keeps >= 256 elements of K: Llama-3.2-1B qkv 4 x 2 (384 WGs), o_proj 4 x 2, down 4 x 4 (512),
   // gate_up 2 x 1 (512), lm_head 1 x 1 (2,004).  One stream at a time uses g_sk (decode is serial).
   static const int target = [] {
@@ -769,9 +772,9 @@ static int launch_mfma(Params p, int tiles, hipStream_t s) {
   auto wgs = [&] { return (int64_t)((tiles + (4 / ks) - 1) / (4 / ks)) * split; };
   while (wgs() < target && (int64_t)ks * split * 2 * 256 <= p.K) {
     if (ks < 4) ks *= 2;
-    else split *= 2;
+    else if (split < kMaxSplit && tiles <= kSkTiles) split *= 2;
+    else break;
   }
-  if (tiles > kSkTiles) split = 1;
   p.split = split;
   const size_t lds = NORM ? (size_t)p.M * p.K * 2 : 0;
   const unsigned grid = (unsigned)wgs();

@@ -642,7 +642,7 @@ def test_dgemv_plain_matches_fp32(M, N, K, path):
         C.dgemv(0, x, None, 0.0, w, y, 0, 0, 0, None, None, None, 1, None, None, None)
         ref = x.float() @ w.float().t()
         assert _rel(y, ref) < 1e-2
-        # split-K launches sum their parts in a device slot they leave zeroed: a repeat is identical
+        # split-K launches sum their parts in a fixed order: a repeat is bit-identical
         y2 = torch.empty_like(y)
         C.dgemv(0, x, None, 0.0, w, y2, 0, 0, 0, None, None, None, 1, None, None, None)
         assert torch.equal(y, y2)
