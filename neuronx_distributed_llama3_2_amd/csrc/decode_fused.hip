@@ -755,7 +755,7 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   }
 }
 
-int g_mfma = -1;   // knob 7: dmm_kernel from this many activation rows on (NXD_DECODE_MFMA; 0 = never)
+int g_mfma = -1;   // knob 7: dmm_kernel from this many activation rows on (NXD_DECODE_MFMA, default 4; 0 = never)
 
 template <int EPI, bool NORM, bool XI>
 static int launch_mfma(Params p, int tiles, hipStream_t s) {
@@ -941,7 +941,7 @@ int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float 
   const bool norm = norm_w != nullptr;
   if (dfused::g_mfma < 0) {
     const char* e = getenv("NXD_DECODE_MFMA");
-    dfused::g_mfma = e ? atoi(e) : 2;
+    dfused::g_mfma = e ? atoi(e) : 4;
   }
   // MFMA rows need whole rotary 8-pair tiles (D / 2 % 8 == 0) and 16-B aligned 32-deep k-steps
   if (M >= 2 && dfused::g_mfma > 0 && M >= dfused::g_mfma && (epi != dfused::ROPE_KV || (D / 2) % 8 == 0))

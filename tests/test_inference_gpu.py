@@ -259,6 +259,55 @@ def test_fused_attention_oproj_matches_two_launches(monkeypatch, hidden, heads, 
     assert ((lf - lu).abs().max() / lu.abs().max()).item() < 2e-2
 
 
+@pytest.mark.parametrize("hidden,heads,batch", [(512, 8, 2), (1024, 8, 4), (2048, 32, 8)])   # D = 64, 128, 64
+def test_fused_decode_mfma_rows_match_valu(monkeypatch, hidden, heads, batch):
+    """decode_fused.hip dmm_kernel (2-8 activation rows on MFMA 16-row weight tiles: QKV + RoPE + KV
+    write, SwiGLU, residual and plain epilogues, k split over waves and workgroups) vs the VALU GEMV
+    body: same greedy tokens, same KV cache, close one-step logits."""
+    from transformers import LlamaConfig, LlamaForCausalLM as HF
+    from neuronx_distributed_llama3_2_amd.inference import model_base
+    from neuronx_distributed_llama3_2_amd.ops import _ext
+
+    C = _ext.ext()
+    cfg = LlamaConfig(hidden_size=hidden, intermediate_size=4 * hidden, num_hidden_layers=2, num_attention_heads=heads,
+                      num_key_value_heads=2, vocab_size=1000, max_position_embeddings=1024, rms_norm_eps=1e-5,
+                      rope_theta=500000.0, tie_word_embeddings=True, eos_token_id=2)
+    torch.manual_seed(0)
+    sd = {k: v.detach().clone() for k, v in HF(cfg).state_dict().items()}
+    torch.manual_seed(7)
+    ids = torch.randint(3, cfg.vocab_size, (batch, 29))
+    monkeypatch.setattr(model_base, "_ATTN_OPROJ", False)   # deterministic attention + o_proj
+    from neuronx_distributed_llama3_2_amd.inference import InferenceConfig, LlamaForCausalLMInference
+    from neuronx_distributed_llama3_2_amd.models.llama.convert import hf_to_nxd
+
+    outs, models = [], []
+    try:
+        for rows in (0, 2):   # VALU body, then MFMA from 2 rows
+            C.decode_set_knob(7, rows)
+            icfg = InferenceConfig(batch_size=batch, seq_len=256, max_context_length=128, use_hip_graphs=False,
+                                   decode_graph_steps=1)
+            m = LlamaForCausalLMInference(cfg, icfg, dtype=torch.bfloat16, device=torch.device("cuda"), init_weights=False)
+            m._load_full(hf_to_nxd(sd, cfg))
+            outs.append(m.generate(ids, max_new_tokens=20, eos_token_id=-1).cpu())
+            assert m.model._decode_fused_ok is True
+            models.append(m)
+        assert torch.equal(outs[0][:, :37], outs[1][:, :37]) and (outs[0] == outs[1]).float().mean() > 0.9
+        kv, km = models[0].model.kv_cache[:, :, :, :, :45].float(), models[1].model.kv_cache[:, :, :, :, :45].float()
+        assert ((kv - km).abs().max() / kv.abs().max()).item() < 3e-2
+        models[1].model.kv_cache.copy_(models[0].model.kv_cache)
+        last = outs[0][:, -1:].cuda()
+        pos = torch.full((batch, 1), outs[0].shape[1] - 1, dtype=torch.int64, device="cuda")
+        sid = torch.arange(batch, device="cuda")
+        clen = torch.full((batch,), outs[0].shape[1], dtype=torch.int32, device="cuda")
+        lg = []
+        for rows, m in zip((0, 2), models):
+            C.decode_set_knob(7, rows)
+            lg.append(m.model.forward_tokens(last, pos, sid, clen).float())
+        assert ((lg[0] - lg[1]).abs().max() / lg[0].abs().max()).item() < 2e-2
+    finally:
+        C.decode_set_knob(7, 4)
+
+
 def test_fused_decode_weight_prefetch_is_exact(monkeypatch):
     """Spare attention workgroups streaming o_proj / gate_up into the Infinity Cache only read:
     decode tokens and logits are bit-identical with and without the prefetch."""

@@ -655,4 +655,4 @@ def test_dgemv_plain_matches_fp32(M, N, K, path):
         assert _rel(yn, h.to(torch.bfloat16).float() @ w.float().t()) < 1e-2
     finally:
         C.decode_set_knob(6, 1)
-        C.decode_set_knob(7, 2)
+        C.decode_set_knob(7, 4)
