@@ -291,7 +291,9 @@ def test_fused_decode_mfma_rows_match_valu(monkeypatch, hidden, heads, batch):
             outs.append(m.generate(ids, max_new_tokens=20, eos_token_id=-1).cpu())
             assert m.model._decode_fused_ok is True
             models.append(m)
-        assert torch.equal(outs[0][:, :37], outs[1][:, :37]) and (outs[0] == outs[1]).float().mean() > 0.9
+        same = (outs[0] == outs[1])
+        assert bool(same[:, :37].all()) and same.float().mean() > 0.9, \
+            f"first mismatch per row: {[int((~r).nonzero()[0]) if (~r).any() else -1 for r in same]}"
         kv, km = models[0].model.kv_cache[:, :, :, :, :45].float(), models[1].model.kv_cache[:, :, :, :, :45].float()
         assert ((kv - km).abs().max() / kv.abs().max()).item() < 3e-2
         models[1].model.kv_cache.copy_(models[0].model.kv_cache)
