@@ -291,21 +291,25 @@ def test_fused_decode_mfma_rows_match_valu(monkeypatch, hidden, heads, batch):
             outs.append(m.generate(ids, max_new_tokens=20, eos_token_id=-1).cpu())
             assert m.model._decode_fused_ok is True
             models.append(m)
-        same = (outs[0] == outs[1])
-        assert bool(same[:, :37].all()) and same.float().mean() > 0.9, \
-            f"first mismatch per row: {[int((~r).nonzero()[0]) if (~r).any() else -1 for r in same]}"
-        kv, km = models[0].model.kv_cache[:, :, :, :, :45].float(), models[1].model.kv_cache[:, :, :, :, :45].float()
-        assert ((kv - km).abs().max() / kv.abs().max()).item() < 3e-2
+        # random-init weights have near-tied logits: greedy generation is judged for consistency
+        # with one full prefill forward of the same model, not for token equality
+        C.decode_set_knob(7, 2)
+        assert _greedy_consistent(models[1], outs[1], 29) > 0.97
+        # one decode step on identical caches: logits and the K / V rows it writes agree
         models[1].model.kv_cache.copy_(models[0].model.kv_cache)
+        n = outs[0].shape[1]
         last = outs[0][:, -1:].cuda()
-        pos = torch.full((batch, 1), outs[0].shape[1] - 1, dtype=torch.int64, device="cuda")
+        pos = torch.full((batch, 1), n - 1, dtype=torch.int64, device="cuda")
         sid = torch.arange(batch, device="cuda")
-        clen = torch.full((batch,), outs[0].shape[1], dtype=torch.int32, device="cuda")
+        clen = torch.full((batch,), n, dtype=torch.int32, device="cuda")
         lg = []
         for rows, m in zip((0, 2), models):
             C.decode_set_knob(7, rows)
             lg.append(m.model.forward_tokens(last, pos, sid, clen).float())
         assert ((lg[0] - lg[1]).abs().max() / lg[0].abs().max()).item() < 2e-2
+        kv = models[0].model.kv_cache[:, :, :, :, n - 1].float()
+        km = models[1].model.kv_cache[:, :, :, :, n - 1].float()
+        assert ((kv - km).abs().max() / kv.abs().max()).item() < 3e-2
     finally:
         C.decode_set_knob(7, 4)
 
