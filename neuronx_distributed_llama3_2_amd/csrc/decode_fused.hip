@@ -654,28 +654,31 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   }
   if (!active) return;
 
-  // ---- split-K across workgroups: every part stores its 16 x 8 partial into its own slot, publishes
-  // it (release) and takes a ticket; the last part sums the slots in part order (the same bits
-  // whichever part arrives last), resets the ticket for the next launch, and runs the epilogue.
-  // No workgroup waits on another.
+  // ---- split-K across workgroups: every part stores its 16 x 8 partial into its own slot with
+  // write-through (sc1) stores, drains them (vmcnt) and takes a ticket (relaxed agent atomic); the
+  // last part reads the slots back with sc1 loads, sums them in part order (the same bits whichever
+  // part arrives last), resets the ticket for the next launch and runs the epilogue.  No fences:
+  // a release fence writes back the whole L2 (buffer_wbl2) and cost the step 0.7 ms at batch 8;
+  // no workgroup waits on another (cdna_hip_programming.md Guideline 16, recipe R1).
   if (p.split > 1) {
     float* sk = g_sk + (int64_t)tile * (kMaxSplit * 128);   // [part][4][32 lanes]
     if (lane < 32) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sk[spi * 128 + 32 * i + lane] = acc[i];
+      for (int i = 0; i < 4; ++i)
+        __hip_atomic_store(sk + spi * 128 + 32 * i + lane, acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int t = 0;
-    if (lane == 0) t = __hip_atomic_fetch_add(g_skc + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) t = __hip_atomic_fetch_add(g_skc + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     t = __shfl(t, 0, 64);
     if (t != p.split - 1) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the ticket
     if (lane < 32) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float v = 0.f;
-        for (int j = 0; j < p.split; ++j) v += sk[j * 128 + 32 * i + lane];
+        for (int j = 0; j < p.split; ++j)
+          v += __hip_atomic_load(sk + j * 128 + 32 * i + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         acc[i] = v;
       }
     }
