@@ -758,32 +758,53 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   }
 }
 
+int g_mfma_split = -1;   // knob 8: K split over workgroups in dmm launches (NXD_DECODE_MFMA_SPLIT, default 0)
 int g_mfma = -1;   // knob 7: dmm_kernel from this many activation rows on (NXD_DECODE_MFMA, default 4; 0 = never)
 
 template <int EPI, bool NORM, bool XI>
 static int launch_mfma(Params p, int tiles, hipStream_t s) {
-  // 4-wave workgroups; K split over KS waves (reduced in LDS) and then over `split` workgroups
-  // (summed in order through g_sk) until ~NXD_DECODE_MFMA_WGS (512) workgroups stream while every wave
-  // keeps >= 256 elements of K: Llama-3.2-1B qkv 4 x 2 (384 WGs), o_proj 4 x 2, down 4 x 4 (512),
-  // gate_up 2 x 1 (512), lm_head 1 x 1 (2,004).  One stream at a time uses g_sk (decode is serial).
+  // K split over KS waves of one workgroup (reduced in LDS), KS doubling until ~2,048 waves stream
+  // while every wave keeps >= 256 elements of K (Llama-3.2-1B: qkv / o_proj 8, down 16, gate_up 2,
+  // lm_head 1), 4 / 8 / 16 waves per workgroup.  NXD_DECODE_MFMA_SPLIT=1 instead keeps 4-wave
+  // workgroups and splits K further over workgroups (hand-off through g_sk) to ~512 workgroups:
+  // batch 8 1.135 vs 1.077 ms per step, batch 4 1.09 vs 1.01 (profiles/r5m_decode_mfma_ab.jsonl).
+  if (g_mfma_split < 0) {
+    const char* e = getenv("NXD_DECODE_MFMA_SPLIT");
+    g_mfma_split = e ? atoi(e) : 0;
+  }
+  const int split_mode = g_mfma_split;
   static const int target = [] {
     const char* e = getenv("NXD_DECODE_MFMA_WGS");
     const int v = e ? atoi(e) : 512;
     return v > 0 ? v : 512;
   }();
-  int ks = 1, split = 1;
-  auto wgs = [&] { return (int64_t)((tiles + (4 / ks) - 1) / (4 / ks)) * split; };
-  while (wgs() < target && (int64_t)ks * split * 2 * 256 <= p.K) {
-    if (ks < 4) ks *= 2;
-    else if (split < kMaxSplit && tiles <= kSkTiles) split *= 2;
-    else break;
-  }
-  p.split = split;
   const size_t lds = NORM ? (size_t)p.M * p.K * 2 : 0;
-  const unsigned grid = (unsigned)wgs();
-  if (ks == 4) hipLaunchKernelGGL((dmm_kernel<EPI, NORM, 4, 4, XI>), dim3(grid), dim3(256), lds, s, p);
-  else if (ks == 2) hipLaunchKernelGGL((dmm_kernel<EPI, NORM, 2, 4, XI>), dim3(grid), dim3(256), lds, s, p);
-  else hipLaunchKernelGGL((dmm_kernel<EPI, NORM, 1, 4, XI>), dim3(grid), dim3(256), lds, s, p);
+  int ks = 1, split = 1;
+  if (split_mode) {
+    auto wgs = [&] { return (int64_t)((tiles + (4 / ks) - 1) / (4 / ks)) * split; };
+    while (wgs() < target && (int64_t)ks * split * 2 * 256 <= p.K) {
+      if (ks < 4) ks *= 2;
+      else if (split < kMaxSplit && tiles <= kSkTiles) split *= 2;
+      else break;
+    }
+    p.split = split;
+    const unsigned grid = (unsigned)wgs();
+    if (ks == 4) hipLaunchKernelGGL((dmm_kernel<EPI, NORM, 4, 4, XI>), dim3(grid), dim3(256), lds, s, p);
+    else if (ks == 2) hipLaunchKernelGGL((dmm_kernel<EPI, NORM, 2, 4, XI>), dim3(grid), dim3(256), lds, s, p);
+    else hipLaunchKernelGGL((dmm_kernel<EPI, NORM, 1, 4, XI>), dim3(grid), dim3(256), lds, s, p);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+  }
+  while (ks < 16 && (int64_t)tiles * ks < 2048 && p.K / (ks * 2) >= 256) ks *= 2;
+  p.split = 1;
+#define NXD_DMM(KSV, NW)                                                                                    \
+  hipLaunchKernelGGL((dmm_kernel<EPI, NORM, KSV, NW, XI>), dim3((unsigned)((tiles + (NW / KSV) - 1) / (NW / KSV))), \
+                     dim3(64 * NW), lds, s, p)
+  if (ks == 16) NXD_DMM(16, 16);
+  else if (ks == 8) NXD_DMM(8, 8);
+  else if (ks == 4) NXD_DMM(4, 4);
+  else if (ks == 2) NXD_DMM(2, 4);
+  else NXD_DMM(1, 4);
+#undef NXD_DMM
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -905,6 +926,7 @@ void dgemv_set_knob(int which, int value) {
   else if (which == 5) dfused::g_occ = value;
   else if (which == 6) dfused::g_dot2 = value != 0;
   else if (which == 7) dfused::g_mfma = value;
+  else if (which == 8) dfused::g_mfma_split = value;
 }
 
 int dgemv_launch(int epi, const void* x, int64_t ldx, const void* norm_w, float eps, const void* w, int64_t ldw, void* y,

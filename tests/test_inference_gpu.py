@@ -259,8 +259,8 @@ def test_fused_attention_oproj_matches_two_launches(monkeypatch, hidden, heads, 
     assert ((lf - lu).abs().max() / lu.abs().max()).item() < 2e-2
 
 
-@pytest.mark.parametrize("hidden,heads,batch", [(512, 8, 2), (1024, 8, 4), (2048, 32, 8)])   # D = 64, 128, 64
-def test_fused_decode_mfma_rows_match_valu(monkeypatch, hidden, heads, batch):
+@pytest.mark.parametrize("hidden,heads,batch,split", [(512, 8, 2, 0), (1024, 8, 4, 0), (2048, 32, 8, 0), (2048, 32, 8, 1)])
+def test_fused_decode_mfma_rows_match_valu(monkeypatch, hidden, heads, batch, split):   # D = 64, 128, 64, 64
     """decode_fused.hip dmm_kernel (2-8 activation rows on MFMA 16-row weight tiles: QKV + RoPE + KV
     write, SwiGLU, residual and plain epilogues, k split over waves and workgroups) vs the VALU GEMV
     body: same greedy tokens, same KV cache, close one-step logits."""
@@ -281,6 +281,7 @@ def test_fused_decode_mfma_rows_match_valu(monkeypatch, hidden, heads, batch):
     from neuronx_distributed_llama3_2_amd.models.llama.convert import hf_to_nxd
 
     outs, models = [], []
+    C.decode_set_knob(8, split)   # K also split over workgroups
     try:
         for rows in (0, 2):   # VALU body, then MFMA from 2 rows
             C.decode_set_knob(7, rows)
@@ -312,6 +313,7 @@ def test_fused_decode_mfma_rows_match_valu(monkeypatch, hidden, heads, batch):
         assert ((kv - km).abs().max() / kv.abs().max()).item() < 3e-2
     finally:
         C.decode_set_knob(7, 4)
+        C.decode_set_knob(8, 0)
 
 
 def test_fused_decode_weight_prefetch_is_exact(monkeypatch):

@@ -626,12 +626,14 @@ def test_rmsnorm_rows_path_vs_fp32(H, T):
 
 @pytest.mark.parametrize("M", [1, 2, 4, 8])
 @pytest.mark.parametrize("N,K", [(2048, 2048), (4096, 8192), (1000, 520)])
-@pytest.mark.parametrize("path", ["fma", "dot2", "mfma"])
+@pytest.mark.parametrize("path", ["fma", "dot2", "mfma", "mfma_split"])
 def test_dgemv_plain_matches_fp32(M, N, K, path):
     """Decode GEMV y = x W^T (PLAIN epilogue, with and without the RMSNorm prologue) on every body:
-    VALU with widened FMAs / v_dot2c_f32_bf16, and the MFMA tiles of 2-8 rows, against fp32."""
+    VALU with widened FMAs / v_dot2c_f32_bf16, and the MFMA tiles of 2-8 rows (K split inside the
+    workgroup, or also over workgroups), against fp32."""
     C = _ext.ext()
-    C.decode_set_knob(7, 2 if path == "mfma" else 0)
+    C.decode_set_knob(7, 2 if path.startswith("mfma") else 0)
+    C.decode_set_knob(8, 1 if path == "mfma_split" else 0)
     dot2 = 0 if path == "fma" else 1
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
@@ -656,3 +658,4 @@ def test_dgemv_plain_matches_fp32(M, N, K, path):
     finally:
         C.decode_set_knob(6, 1)
         C.decode_set_knob(7, 4)
+        C.decode_set_knob(8, 0)
