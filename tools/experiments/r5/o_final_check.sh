@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 5 O: end-of-round check on one MI355X -- the whole GPU suite (durations), smoke(), a 1-GPU bench
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r5o
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread --durations=25 > $O/pytest.log 2>&1
+rc=$?
+tail -3 $O/pytest.log
+grep -E "FAILED|ERROR" $O/pytest.log | head
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python -u bench.py --steps 10 --warmup 3 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+tail -1 $O/bench.json
