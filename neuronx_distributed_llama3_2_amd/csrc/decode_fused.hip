@@ -462,7 +462,7 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   __shared__ float red[NWV][8];
   __shared__ f32x4_t part[KS > 1 ? NWV : 1][32];
   constexpr int G = NWV / KS;
-  constexpr int U = 8;                                 // 32-deep k-steps per load round
+  constexpr int U = 4;                                 // 32-deep k-steps per load round (two rounds in flight)
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int rg = wid / KS, ks = wid % KS;
   const int spi = (int)blockIdx.x % p.split;            // this workgroup's K part of its tiles
@@ -498,14 +498,15 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   const int kc = ((p.K + nparts - 1) / nparts + 31) & ~31;
   const int kbeg = min((spi * KS + ks) * kc, p.K), kend = min(p.K, kbeg + kc);
   const int kq = 8 * (lane >> 4);                      // this lane's k offset inside a 32-step
-  u32x4_t wv[U];
-  auto load_round = [&](int base) {
+  u32x4_t wv[U], wn[U];   // double-buffered weight rounds: round r + 1 is in flight while r is consumed
+  auto load_into = [&](u32x4_t (&dst)[U], int base) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = min(base + 32 * u + kq, kend - 8);
-      wv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(wrow + k));
+      dst[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(wrow + k));
     }
   };
+  auto load_round = [&](int base) { load_into(wv, base); };
   auto xrow = [&](int m) -> const uint16_t* {
     if constexpr (XI) {
       const int64_t t = p.xidx[m];
@@ -534,6 +535,7 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
     for (int m = 0; m < 8; ++m) xpre[m] = *reinterpret_cast<const u32x4_t*>(xrow(min(m, p.M - 1)) + k);
   }
   if (kbeg < kend) load_round(kbeg);
+  if (kbeg + 32 * U < kend) load_into(wn, kbeg + 32 * U);
   // epilogue operands (residual row + pending fp32 sum; rotary position + cos / sin) issued now,
   // so they land behind the first weight round instead of as round trips after the reduction
   const int m0 = 4 * (lane >> 4);
@@ -624,20 +626,36 @@ __global__ void __launch_bounds__(64 * NWV, 4) dmm_kernel(Params p) {
   // unpredicated load; a predicated one made hipcc spill the whole round)
   const uint16_t* xr = NORM ? xs + min(c, p.M - 1) * p.K : p.x + (int64_t)min(c, p.M - 1) * p.ldx;
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int base = kbeg; base < kend; base += 32 * U) {
-    if (base != kbeg) load_round(base);
-    u32x4_t xa[U];
+  // two weight rounds in flight: rounds 0 and 1 went out before the prologue; after the MFMAs of
+  // round r its buffer takes round r + 2.  The activation chunks of round r + 1 are issued before
+  // the weights of round r + 2 (vmcnt retires in order: waiting for them never waits for weights)
+  auto load_x = [&](u32x4_t (&xa)[U], int base) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = base + 32 * u + kq;
       const u32x4_t v = *reinterpret_cast<const u32x4_t*>(xr + min(k, kend - 8));
       xa[u] = (arow && k < kend) ? v : u32x4_t{0u, 0u, 0u, 0u};
     }
+  };
+  auto mfma_round = [&](const u32x4_t (&w)[U], const u32x4_t (&xa)[U], int base) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (base + 32 * u < kend)   // wave-uniform
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, xa[u]), __builtin_bit_cast(bf16x8_t, wv[u]), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, xa[u]), __builtin_bit_cast(bf16x8_t, w[u]), acc, 0, 0, 0);
+    }
+  };
+  constexpr int RK = 32 * U;   // k per round
+  u32x4_t xc[U], xn[U];
+  if (kbeg < kend) load_x(xc, kbeg);
+#pragma unroll 1
+  for (int base = kbeg; base < kend; base += 2 * RK) {
+    mfma_round(wv, xc, base);
+    if (base + RK < kend) load_x(xn, base + RK);
+    if (base + 2 * RK < kend) load_into(wv, base + 2 * RK);
+    if (base + RK < kend) {
+      mfma_round(wn, xn, base + RK);
+      if (base + 2 * RK < kend) load_x(xc, base + 2 * RK);
+      if (base + 3 * RK < kend) load_into(wn, base + 3 * RK);
     }
   }
 

@@ -15,7 +15,6 @@ for rep in 1 2; do
   for bs in 2 4 8; do
     run valu_dot2 $bs NXD_DECODE_MFMA=0
     run mfma $bs NXD_DECODE_MFMA=2
-    run mfma_split $bs NXD_DECODE_MFMA=2 NXD_DECODE_MFMA_SPLIT=1
   done
 done
 true
