@@ -2,7 +2,7 @@
 # round 5 O: end-of-round check on one MI355X -- the whole GPU suite (durations), smoke(), a 1-GPU bench
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/r5o
+O=gpurun_out/${R5O_DIR:-r5o}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread --durations=25 > $O/pytest.log 2>&1
