@@ -10,8 +10,13 @@
 //
 // Per rank, one IPC-exported region: a 4 KiB header of flags [2][kMaxBlocks] (uint64 epochs) + slots
 // [2][nmax x 4 B].
-// Call c of a rank has epoch e = ctr[b] + 1 (per-block device counter, so hipGraph replays keep
-// counting) and parity e & 1.  Block b of every rank:
+// Call c of a rank has epoch e = ctr[0] + 1 (one device counter per rank, advanced by the last block of
+// the call to finish -- an arrival ticket in ctr[1] -- so hipGraph replays keep counting) and parity
+// e & 1; every block of a call uses the same epoch.  (Per-block counters broke the slot-reuse argument
+// below once calls of different sizes, hence different block-to-chunk maps, alternate: a block's
+// parity then no longer alternated with the call, and a rank could overwrite a slot region a peer
+// was still reading for the previous call -- a reduce-scatter mismatch in the 4-rank GPU test.)
+// Block b of every rank:
 //   1. copies its chunk of the local partial into slot[parity] (and zeroes the partial when it is an
 //      atomic accumulator that must start at zero for the next producer);
 //   2. publishes: every wave drains its stores (vmcnt(0)), workgroup barrier, one system-scope release
@@ -22,7 +27,8 @@
 //   4. sums the W chunks in rank order (bitwise identical on every rank: the residual stream stays
 //      replicated) and applies the epilogue.
 // A slot is rewritten two calls later; by then every peer has passed the intervening call, which it
-// only enters after finishing its reads of this one, so two slots suffice.
+// only enters after finishing its reads of this one (kernel order on its stream), so two slots
+// suffice.
 #include "common.h"
 
 #include <cstdio>
@@ -46,7 +52,7 @@ struct Args {
   const float* peer_slot[kMaxRanks][2];      // every rank's slots (own included), as mapped here
   uint64_t* flag;                            // this rank's flags [2][kMaxBlocks] (IPC region)
   const uint64_t* peer_flag[kMaxRanks];      // every rank's flags, as mapped here
-  uint64_t* ctr;                             // [kMaxBlocks] epochs (local memory)
+  uint64_t* ctr;                             // [0] epoch of the last call, [1] arrival ticket (local memory)
   int* err;                                  // > 0: a peer never arrived (bounded spin expired)
   int world, rank, n, chunk, mode;
   int64_t spin_limit;
@@ -58,11 +64,21 @@ struct Args {
   int rowu;
 };
 
+// The last block of a call to finish (arrival ticket) publishes the call's epoch for the next call.
+// Every block read ctr[0] at its start, before taking its ticket, so none reads the new value.
+__device__ __forceinline__ void advance_epoch(uint64_t* ctr, uint64_t e) {
+  const uint64_t t = __hip_atomic_fetch_add(ctr + 1, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == gridDim.x - 1) {
+    __hip_atomic_store(ctr + 1, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ctr, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
   __shared__ uint64_t e_s;
   const int b = blockIdx.x, tid = threadIdx.x;
   const int lo = b * a.chunk, hi = min(a.n, lo + a.chunk);
-  if (tid == 0) e_s = a.ctr[b] + 1;
+  if (tid == 0) e_s = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   __syncthreads();
   const uint64_t e = e_s;
   const int par = (int)(e & 1);
@@ -121,7 +137,7 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
         }
       }
     }
-    if (tid == 0) a.ctr[b] = e;
+    if (tid == 0) advance_epoch(a.ctr, e);
     return;
   }
   for (int i = lo + tid; i < hi; i += kThreads) {
@@ -139,7 +155,7 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
       a.res[i] = f2bf(s);
     }
   }
-  if (tid == 0) a.ctr[b] = e;
+  if (tid == 0) advance_epoch(a.ctr, e);
 }
 
 struct Handle {
@@ -190,7 +206,7 @@ __global__ void __launch_bounds__(kThreads) peer_coll_kernel(CollArgs a) {
   __shared__ uint64_t e_s;
   const int b = blockIdx.x, tid = threadIdx.x;
   const int64_t lo = (int64_t)b * a.chunk, hi = min(a.n, lo + a.chunk);
-  if (tid == 0) e_s = a.ctr[b] + 1;
+  if (tid == 0) e_s = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   __syncthreads();
   const uint64_t e = e_s;
   const int par = (int)(e & 1);
@@ -266,7 +282,7 @@ __global__ void __launch_bounds__(kThreads) peer_coll_kernel(CollArgs a) {
       }
     }
   }
-  if (tid == 0) a.ctr[b] = e;
+  if (tid == 0) advance_epoch(a.ctr, e);
 }
 
 }  // namespace par
