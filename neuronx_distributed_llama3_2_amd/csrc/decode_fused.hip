@@ -146,9 +146,10 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
   // only be waited for together with all of them: the prologue then started only once the weights
   // had landed, and its own L2 round trip and barriers were added to every wave's critical path.
   // (Left uninitialised where not loaded; only read under the same conditions.)
-  constexpr bool PRE = NORM && MM == 1;
-  u32x4_t x0, gw0 = {0, 0, 0, 0};
-  f32x4_t xa0, xa1;
+  // (Rows of bs <= 2 too: at 2 rows the prologue behind the weights cost gate_up / qkv 2-4 us each.)
+  constexpr bool PRE = NORM && MM <= 2;
+  u32x4_t x0[MM], gw0 = {0, 0, 0, 0};
+  f32x4_t xa0[MM], xa1[MM];
   const bool pre_ok = PRE && tid * 8 < p.K;
   // XI: input row m is an embedding-table row picked by a token id (a scalar load).  Its gather is
   // still issued ahead of the weights: waiting for the id delays the weight round by one scalar
@@ -174,10 +175,14 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
     }
   };
   if (pre_ok) {
-    x0 = *reinterpret_cast<const u32x4_t*>(xrow(0) + tid * 8);
-    if (p.xadd) {
-      xa0 = *reinterpret_cast<const f32x4_t*>(p.xadd + tid * 8);
-      xa1 = *reinterpret_cast<const f32x4_t*>(p.xadd + tid * 8 + 4);
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {   // rows past M re-read the last row (never used)
+      const int mm = min(m, p.M - 1);
+      x0[m] = *reinterpret_cast<const u32x4_t*>(xrow(mm) + tid * 8);
+      if (p.xadd) {
+        xa0[m] = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)mm * p.K + tid * 8);
+        xa1[m] = *reinterpret_cast<const f32x4_t*>(p.xadd + (int64_t)mm * p.K + tid * 8 + 4);
+      }
     }
     gw0 = *reinterpret_cast<const u32x4_t*>(p.norm_w + tid * 8);
   }
@@ -237,8 +242,8 @@ __device__ __forceinline__ void dgemv_body(const Params& p) {
           u32x4_t v;
           f32x4_t a0, a1;
           if (PRE && k == tid * 8) {   // the chunk loaded ahead of the weights
-            v = x0;
-            if (p.xadd) { a0 = xa0; a1 = xa1; }
+            v = x0[m];
+            if (p.xadd) { a0 = xa0[m]; a1 = xa1[m]; }
           } else {
             v = *reinterpret_cast<const u32x4_t*>(xrow(m) + k);
             if (p.xadd) {
