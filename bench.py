@@ -189,6 +189,28 @@ class _Child:
         return "\n".join(self.tail)[-n_chars:]
 
 
+def _per_rank_seconds(name: str, default: str, rank: int) -> float:
+    """A watchdog limit: one number for every rank, or a comma list indexed by rank (the last entry
+    covers the higher ranks) -- tests give the rank that hangs the shortest limit."""
+    vals = [float(v) for v in os.environ.get(name, default).split(",") if v.strip()]
+    return vals[min(rank, len(vals) - 1)]
+
+
+def _failure_record(k: int, name: str, knobs, rc: int, why: str, t_rung: float, first_rank, tails, killed):
+    """One failed rung for the JSON history.  `first_rank` is the rank whose exit (non-zero, or its
+    own watchdog's 124) ended the rung -- its stderr tail is the diagnosis.  Ranks the supervisor
+    killed afterwards are listed apart with their tails: they are collateral, not the cause.  With no
+    first rank (the rung's wall budget ran out) every rank was killed and every tail is kept."""
+    rec = {"rung": k, "name": name, "knobs": knobs, "rc": rc, "why": why, "s": round(time.monotonic() - t_rung, 1),
+           "failed_rank": first_rank, "killed_by_supervisor": sorted(killed),
+           "killed_tails": {str(r): tails.get(r, "") for r in sorted(killed) if r != first_rank}}
+    if first_rank is not None:
+        rec["stderr_tail"] = tails.get(first_rank, "")
+    else:
+        rec["stderr_tail"] = "\n".join(f"[rank {r}] {t}" for r, t in sorted(tails.items()))[-3000:]
+    return rec
+
+
 def _rung_deadline(t_start: float, k: int) -> float:
     """Wall deadline of rung k (1-based): the budget minus what the later rungs keep in reserve."""
     return t_start + LADDER_BUDGET_S - (len(LADDER) - k) * LADDER_MIN_RUNG_S
@@ -219,12 +241,13 @@ def launch_local_ranks(argv, n: int) -> int:
                 for r in range(n)]
         deadline = _rung_deadline(t0, k)
         t_rung = time.monotonic()
-        why, rc = None, 0
+        why, rc, first = None, 0, None
         while True:
             codes = [c.poll() for c in kids]
             bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
             if bad:
                 r, c = bad[0]
+                first = r
                 rc = c if c > 0 else 128 - c
                 why = f"rank {r} exited {c}"
                 break
@@ -238,6 +261,7 @@ def launch_local_ranks(argv, n: int) -> int:
             grace = time.monotonic() + 20.0      # rank 0 is done: the others are in their final barrier
             while any(c.poll() is None for c in kids) and time.monotonic() < grace:
                 time.sleep(0.2)
+        killed = [r for r, c in enumerate(kids) if c.poll() is None]   # still running: the supervisor ends them
         for c in kids:
             c.kill()
         if why is None and kids[0].json_lines:
@@ -245,9 +269,10 @@ def launch_local_ranks(argv, n: int) -> int:
             return 0
         if why is None:
             rc, why = 1, "rank 0 exited 0 without a result line"
-        tails = {r: c.tail_text() for r, c in enumerate(kids) if c.poll() not in (None, 0)}
-        history.append({"rung": k, "name": name, "knobs": knobs, "rc": rc, "why": why,
-                        "s": round(time.monotonic() - t_rung, 1), "stderr_tail": tails.get(0) or next(iter(tails.values()), "")})
+        if first is None and why.startswith("rank 0 exited 0"):
+            first = 0
+        tails = {r: c.tail_text() for r, c in enumerate(kids)}
+        history.append(_failure_record(k, name, knobs, rc, why, t_rung, first, tails, killed))
         sys.stderr.write(f"[bench] ladder rung {k} ({name}) failed: {why}\n")
         sys.stderr.flush()
     return rc
@@ -282,13 +307,14 @@ def supervise_launched_rank(argv) -> int:
         child = _Child(argv, _rung_env(env, k, knobs), hold_json=(rank == 0))
         deadline = _rung_deadline(t0, k)
         t_rung = time.monotonic()
-        why, rc, done_seen = None, 0, None
+        why, rc, done_seen, order = None, 0, None, 0
         while True:
             c = child.poll()
             if c is not None and c != 0:
                 if rank != 0 and store.check([_PFX + "done"]):
                     break   # rank 0 already reported this rung's result (a late teardown failure here)
                 rc, why = (c if c > 0 else 128 - c), f"rank {rank} exited {c}"
+                order = store.add(key + "order", 1)   # 1 = this rank failed first
                 store.set(key + "fail", why)
                 break
             if c == 0:
@@ -310,14 +336,17 @@ def supervise_launched_rank(argv) -> int:
             time.sleep(0.2)
         if why is None and rank == 0 and not child.json_lines:
             rc, why = 1, "rank 0 exited 0 without a result line"
+            order = store.add(key + "order", 1)
             store.set(key + "fail", why)
+        killed = child.poll() is None   # this supervisor ends a still-running child: collateral
         child.kill()
         if why is None:
             if rank == 0:
                 store.set(_PFX + "done", str(k))
                 _emit(child.json_lines[-1], k, history)
             return 0
-        store.set(key + f"end/{rank}", json.dumps({"rc": rc, "why": why, "tail": child.tail_text()}))
+        store.set(key + f"end/{rank}", json.dumps({"rc": rc, "why": why, "tail": child.tail_text(),
+                                                   "order": order, "killed": killed}))
         # every rank's child of this rung is dead before anyone starts the next rung
         try:
             store.wait([key + f"end/{r}" for r in range(world)], timedelta(seconds=60))
@@ -330,10 +359,13 @@ def supervise_launched_rank(argv) -> int:
                     ends[r] = json.loads(store.get(key + f"end/{r}").decode())
             except Exception:
                 pass
-        first = next((e for e in ends.values() if not e["why"].startswith("peer:")), ends.get(rank, {}))
-        history.append({"rung": k, "name": name, "knobs": knobs, "rc": first.get("rc", rc),
-                        "why": first.get("why", why), "s": round(time.monotonic() - t_rung, 1),
-                        "stderr_tail": first.get("tail", "")})
+        # the rank that failed first (lowest arrival order on the store); none when the budget ran out
+        failed = sorted((e["order"], r) for r, e in ends.items() if e.get("order", 0) > 0)
+        first_rank = failed[0][1] if failed else None
+        first = ends.get(first_rank, ends.get(rank, {}))
+        history.append(_failure_record(k, name, knobs, first.get("rc", rc), first.get("why", why), t_rung, first_rank,
+                                       {r: e.get("tail", "") for r, e in ends.items()},
+                                       [r for r, e in ends.items() if e.get("killed")]))
         if rank == 0:
             sys.stderr.write(f"[bench] ladder rung {k} ({name}) failed: {history[-1]['why']}\n")
             sys.stderr.flush()
@@ -452,8 +484,8 @@ def main(a):
     # instead of hanging every rank; the host watchdog below catches what that does not.  The first
     # optimizer step (startup, GEMM autotuning) gets NXD_BENCH_WATCHDOG_S, every later one
     # NXD_BENCH_STEP_WATCHDOG_S, so a hang after step 1 leaves the ladder time for its next rungs.
-    wd_s = float(os.environ.get("NXD_BENCH_WATCHDOG_S", "240"))
-    wd_step_s = float(os.environ.get("NXD_BENCH_STEP_WATCHDOG_S", "90"))
+    wd_s = _per_rank_seconds("NXD_BENCH_WATCHDOG_S", "240", rank)
+    wd_step_s = _per_rank_seconds("NXD_BENCH_STEP_WATCHDOG_S", "90", rank)
     coll_timeout = configure_collective_watchdog(2 * wd_s if wd_s > 0 else 1800.0)
     dist.init_process_group(backend, rank=rank, world_size=world, timeout=coll_timeout,
                             device_id=torch.device("cuda", local_rank) if use_cuda and backend == "nccl" else None)

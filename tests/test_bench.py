@@ -153,3 +153,26 @@ def test_bench_ladder_rung_budget_kills_silent_hang():
     rec = _json_lines(r.stdout)[0]
     assert rec["attempt"] == 2 and rec["ladder_failed"][0]["rc"] == 124
     assert "wall budget" in rec["ladder_failed"][0]["why"]
+
+
+@pytest.mark.parametrize("launcher", ["self", "torchrun"])
+def test_bench_ladder_names_the_hung_rank(launcher):
+    """Rank 1 hangs and its own (short) step watchdog ends it; rank 0, blocked in a collective with a
+    long watchdog, is killed by the supervisor.  The history must blame rank 1 -- its tail carries the
+    watchdog's flight-recorder dump -- and list rank 0 as collateral, not as the failure."""
+    env = _env()
+    env.update(NXD_BENCH_LADDER_FAULTS="1=bench_microstep@1#2:hang", NXD_BENCH_WATCHDOG_S="60",
+               NXD_BENCH_STEP_WATCHDOG_S="120,15")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", *ARGS]
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", "29634", "bench.py", "--gpus", "2", *ARGS]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["attempt"] == 2
+    f = rec["ladder_failed"][0]
+    assert f["failed_rank"] == 1 and f["rc"] == 124, f
+    assert "last collectives issued" in f["stderr_tail"], f
+    assert f["killed_by_supervisor"] == [0], f
+    assert "0" in f["killed_tails"]
