@@ -76,6 +76,9 @@ int grouped_rowgemm_launch(int, const void*, const void*, void*, const int*, int
 int wgrad_gemm_grouped_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int64_t, const int*, int, int,
                               int, int, hipStream_t);
 void wgrad_gemm_set_ablate(int);
+int dense_gemm_launch(int, int, const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, hipStream_t);
+int dense_gemm_choose_splits(int, int, int);
+void dense_gemm_set_pipe(int);
 void grouped_rowgemm_set_pp(int);
 void wgrad_gemm_set_pp(int);
 int cu_stream_launch(const void*, void*, int64_t, int, int64_t, hipStream_t);
@@ -742,6 +745,41 @@ void wgrad_gemm(at::Tensor mg, at::Tensor dy, at::Tensor x, int64_t splits) {
            "wgrad_gemm");
 }
 
+// Hand-written dense GEMM (csrc/dense_gemm.hip).  layout 0 (NT): c[M, N] = a[M, K] b[N, K]^T;
+// layout 1 (TN): c[M, N] = a[K, M]^T b[K, N] (token-major weight gradient).  epi 0: c bf16 = result;
+// 1: c fp32 += result (deterministic); 2: c fp32 += result by split-K atomics (splits <= 0: chosen).
+void dense_gemm(int64_t layout, int64_t epi, at::Tensor a, at::Tensor b, at::Tensor c, int64_t splits) {
+  check_bf16(a, "dense_gemm a");
+  check_bf16(b, "dense_gemm b");
+  check_cuda(c, "dense_gemm c");
+  TORCH_CHECK(layout == 0 || layout == 1, "dense_gemm: layout must be 0 (NT) or 1 (TN)");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "dense_gemm: epi must be 0, 1 or 2");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "dense_gemm: 2-D operands");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "dense_gemm: unit inner strides");
+  TORCH_CHECK(c.scalar_type() == (epi == 0 ? at::kBFloat16 : at::kFloat), "dense_gemm: c dtype must be ",
+              epi == 0 ? "bfloat16" : "float32");
+  int64_t M, N, K;
+  if (layout == 0) {
+    M = a.size(0); K = a.size(1); N = b.size(0);
+    TORCH_CHECK(b.size(1) == K, "dense_gemm NT: a [M, K], b [N, K]");
+  } else {
+    K = a.size(0); M = a.size(1); N = b.size(1);
+    TORCH_CHECK(b.size(0) == K, "dense_gemm TN: a [K, M], b [K, N]");
+    TORCH_CHECK(M % 8 == 0, "dense_gemm TN: M % 8 must be 0");
+  }
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "dense_gemm: c must be [M, N]");
+  TORCH_CHECK(K % 64 == 0 && N % 8 == 0, "dense_gemm: K % 64 and N % 8 must be 0");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % (epi == 0 ? 8 : 4) == 0,
+              "dense_gemm: row strides must be multiples of 8 elements (c fp32: 4)");
+  TORCH_CHECK(M <= INT32_MAX && N <= INT32_MAX && K <= INT32_MAX, "dense_gemm: dims too large");
+  check_aligned16(a, "dense_gemm a");
+  check_aligned16(b, "dense_gemm b");
+  check_aligned16(c, "dense_gemm c");
+  check_rc(nxd::dense_gemm_launch((int)layout, (int)epi, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+                                  c.data_ptr(), c.stride(0), (int)M, (int)N, (int)K, (int)splits, cur_stream()),
+           "dense_gemm");
+}
+
 // MoE grouped GEMMs over expert-sorted rows (csrc/grouped_gemm.hip); offs int32 [E + 1] on device.
 //   mode 0: a = x [M, K], b = W [E, K, N], c = y [M, N] bf16
 //   mode 1: a = dy [M, N], b = W [E, K, N], c = dx [M, K] bf16
@@ -1021,6 +1059,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("expert_gemv", &expert_gemv);
   m.def("grouped_gemm", &grouped_gemm);
   m.def("wgrad_gemm", &wgrad_gemm);
+  m.def("dense_gemm", &dense_gemm, py::arg("layout"), py::arg("epi"), py::arg("a"), py::arg("b"), py::arg("c"),
+        py::arg("splits") = 0);
+  m.def("dense_gemm_set_pipe", [](int64_t v) { nxd::dense_gemm_set_pipe((int)v); });
+  m.def("dense_gemm_splits", [](int64_t M, int64_t N, int64_t K) {
+    return nxd::dense_gemm_choose_splits((int)M, (int)N, (int)K);
+  });
   // diagnostics: copy kernel on exactly `blocks` workgroups (CU-interference measurements)
   // A HIP stream whose kernels may only use the CUs whose bits are NOT listed in `exclude`
   // (hipExtStreamCreateWithCUMask; the CUs left out stay free for the collectives' kernels, which

@@ -22,8 +22,11 @@
 //   2. publishes: every wave drains its stores (vmcnt(0)), workgroup barrier, one system-scope release
 //      (the region may be read from another GPU over xGMI), then the flag[parity][b] = e store;
 //   3. waits for flag[parity][b] >= e of every peer (relaxed system-scope polls with s_sleep and a
-//      bounded spin -- an absent peer sets *err and the kernel still exits), then one system-scope
-//      acquire and a barrier;
+//      bounded spin), then one system-scope acquire and a barrier.  A peer that never arrives, or whose
+//      flag is PAST e (it skipped a call: the two ranks' call sequences diverged), marks the call
+//      lost: *err (pinned host memory, read by the host without a sync) is set, every output of the
+//      call is written as NaN (a missed check cannot pass stale slots off as a sum) and the rank's
+//      flags are poisoned so its peers fail their next call as well;
 //   4. sums the W chunks in rank order (bitwise identical on every rank: the residual stream stays
 //      replicated) and applies the epilogue.
 // A slot is rewritten two calls later; by then every peer has passed the intervening call, which it
@@ -53,7 +56,7 @@ struct Args {
   uint64_t* flag;                            // this rank's flags [2][kMaxBlocks] (IPC region)
   const uint64_t* peer_flag[kMaxRanks];      // every rank's flags, as mapped here
   uint64_t* ctr;                             // [0] epoch of the last call, [1] arrival ticket (local memory)
-  int* err;                                  // > 0: a peer never arrived (bounded spin expired)
+  int* err;                                  // != 0: a peer never arrived / diverged (host-mapped)
   int world, rank, n, chunk, mode;
   int64_t spin_limit;
   float* out;                                // SUM: [n] fp32
@@ -74,8 +77,30 @@ __device__ __forceinline__ void advance_epoch(uint64_t* ctr, uint64_t e) {
   }
 }
 
+// Poll a peer's flag for epoch e.  Legal values are e - 2 (the peer has not reached this call yet)
+// and e (published); anything past e means the peer skipped a call (or this rank did).  Returns false
+// for a lost peer: bounded spin expired or a diverged epoch.
+__device__ __forceinline__ bool wait_peer(const uint64_t* pf, uint64_t e, int64_t spin_limit) {
+  int64_t it = 0;
+  uint64_t v;
+  while ((v = __hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) < e) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++it > spin_limit) return false;
+  }
+  return v == e;
+}
+
+// A rank that lost a peer poisons ALL its flags (both parities, every block): a peer still running
+// (or one that comes back late) then reads a value past its epoch on its next wait and fails that call
+// too, instead of summing this rank's stale slot as if the sequences still matched.
+__device__ __forceinline__ void poison_flags(uint64_t* flag, int tid) {
+  static_assert(kThreads >= 2 * kMaxBlocks, "one flag per thread");
+  if (tid < 2 * kMaxBlocks) __hip_atomic_store(flag + tid, ~(uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
   __shared__ uint64_t e_s;
+  __shared__ int lost_s;
   const int b = blockIdx.x, tid = threadIdx.x;
   const int lo = b * a.chunk, hi = min(a.n, lo + a.chunk);
   if (tid == 0) e_s = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
@@ -108,17 +133,15 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
 #pragma unroll
   for (int r = 0; r < kMaxRanks; ++r)
     if (r == tid) pf = a.peer_flag[r] + par * kMaxBlocks + b;
-  if (tid < a.world && tid != a.rank) {
-    int64_t it = 0;
-    while (__hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++it > a.spin_limit) {
-        atomicAdd(a.err, 1);
-        break;
-      }
-    }
+  if (tid == 0) lost_s = 0;
+  __syncthreads();
+  if (tid < a.world && tid != a.rank && !wait_peer(pf, e, a.spin_limit)) {
+    lost_s = 1;
+    __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
+  const bool lost = lost_s != 0;
+  if (lost) poison_flags(a.flag, tid);
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -132,7 +155,8 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < kMaxRanks; ++r) {
         if (r < a.world) {
-          const u32x4_t v = reinterpret_cast<const u32x4_t*>(par ? a.peer_slot[r][1] : a.peer_slot[r][0])[u];
+          u32x4_t v = reinterpret_cast<const u32x4_t*>(par ? a.peer_slot[r][1] : a.peer_slot[r][0])[u];
+          if (lost) v = u32x4_t{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};   // NaN in bf16 and fp32
           reinterpret_cast<u32x4_t*>(a.out)[((int64_t)m * a.world + r) * a.rowu + j] = v;
         }
       }
@@ -145,12 +169,13 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
 #pragma unroll
     for (int r = 0; r < kMaxRanks; ++r)
       if (r < a.world) s += (par ? a.peer_slot[r][1] : a.peer_slot[r][0])[i];
+    if (lost) s = __builtin_nanf("");
     if (a.mode == SUM) {
       a.out[i] = s;
     } else if (a.mode == FOLD_RES) {
       // the unfused TP = 1 rounding: y = bf16(bf16(y + bf16(o_proj)) + bf16(down))
       const float y = bf2f(f2bf(bf2f(a.res[i]) + bf2f(f2bf(a.xadd[i]))));
-      a.res[i] = f2bf(y + bf2f(f2bf(s)));
+      a.res[i] = lost ? (uint16_t)0xFFFF : f2bf(y + bf2f(f2bf(s)));
     } else {
       a.res[i] = f2bf(s);
     }
@@ -167,7 +192,8 @@ struct Handle {
   char* peer_base[kMaxRanks] = {};
   bool opened[kMaxRanks] = {};
   uint64_t* ctr = nullptr;
-  int* err = nullptr;
+  int* err = nullptr;          // device-side pointer the kernels store to
+  int* err_host = nullptr;     // the same word, host-mapped pinned memory (nullptr: device memory)
 };
 
 constexpr size_t kFlagBytes = 2 * kMaxBlocks * sizeof(uint64_t);
@@ -204,6 +230,7 @@ __device__ __forceinline__ void copy16(const char* src, char* dst, int64_t b0, i
 
 __global__ void __launch_bounds__(kThreads) peer_coll_kernel(CollArgs a) {
   __shared__ uint64_t e_s;
+  __shared__ int lost_s;
   const int b = blockIdx.x, tid = threadIdx.x;
   const int64_t lo = (int64_t)b * a.chunk, hi = min(a.n, lo + a.chunk);
   if (tid == 0) e_s = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
@@ -229,17 +256,15 @@ __global__ void __launch_bounds__(kThreads) peer_coll_kernel(CollArgs a) {
 #pragma unroll
   for (int r = 0; r < kMaxRanks; ++r)
     if (r == tid) pf = a.peer_flag[r] + par * kMaxBlocks + b;
-  if (tid < a.world && tid != a.rank) {
-    int64_t it = 0;
-    while (__hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++it > a.spin_limit) {
-        atomicAdd(a.err, 1);
-        break;
-      }
-    }
+  if (tid == 0) lost_s = 0;
+  __syncthreads();
+  if (tid < a.world && tid != a.rank && !wait_peer(pf, e, a.spin_limit)) {
+    lost_s = 1;
+    __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
+  const bool lost = lost_s != 0;
+  if (lost) poison_flags(a.flag, tid);
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -251,7 +276,8 @@ __global__ void __launch_bounds__(kThreads) peer_coll_kernel(CollArgs a) {
       if (r < a.world) {
         const char* src = par ? a.peer_slot[r][1] : a.peer_slot[r][0];
         for (int64_t o = lo * a.es + (int64_t)tid * 16; o < hi * a.es; o += (int64_t)kThreads * 16)
-          *reinterpret_cast<u32x4_t*>(a.out + (int64_t)r * a.n * a.es + o) = *reinterpret_cast<const u32x4_t*>(src + o);
+          *reinterpret_cast<u32x4_t*>(a.out + (int64_t)r * a.n * a.es + o) =
+              lost ? u32x4_t{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu} : *reinterpret_cast<const u32x4_t*>(src + o);
       }
     }
   } else {
@@ -274,6 +300,10 @@ __global__ void __launch_bounds__(kThreads) peer_coll_kernel(CollArgs a) {
             for (int j = 0; j < 4; ++j) acc[j] += __uint_as_float(v[j]);
           }
         }
+      }
+      if (lost) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = __builtin_nanf("");
       }
       if (a.es == 2) {
         *reinterpret_cast<u32x4_t*>(a.out + i * 2) = pack8(acc);
@@ -316,8 +346,28 @@ void* peer_ar_create(int64_t nmax, int* uncached) {
   }
   h->base = static_cast<char*>(p);
   if (hipMemset(h->base, 0, h->bytes) != hipSuccess || hipMalloc(&h->ctr, par::kMaxBlocks * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(h->ctr, 0, par::kMaxBlocks * sizeof(uint64_t)) != hipSuccess || hipMalloc(&h->err, sizeof(int)) != hipSuccess ||
-      hipMemset(h->err, 0, sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      hipMemset(h->ctr, 0, par::kMaxBlocks * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    delete h;
+    return nullptr;
+  }
+  // the lost-peer word in pinned, host-mapped memory: the host reads it after any step without a
+  // device sync or a copy (device memory + hipMemcpy if the runtime refuses the mapping)
+  void* hp = nullptr;
+  if (hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, hp, 0) == hipSuccess) {
+      h->err_host = static_cast<int*>(hp);
+      h->err = static_cast<int*>(dp);
+      *reinterpret_cast<volatile int*>(h->err_host) = 0;
+    } else {
+      (void)hipGetLastError();
+      (void)hipHostFree(hp);
+    }
+  } else {
+    (void)hipGetLastError();
+  }
+  if (!h->err && (hipMalloc(&h->err, sizeof(int)) != hipSuccess || hipMemset(h->err, 0, sizeof(int)) != hipSuccess ||
+                  hipDeviceSynchronize() != hipSuccess)) {
     delete h;
     return nullptr;
   }
@@ -433,11 +483,21 @@ int peer_coll_run(void* hv, const void* in, void* out, int64_t n, int es, int mo
   return (int)hipGetLastError();
 }
 
+// Non-zero once any call of this handle lost a peer.  Pinned word: reflects every call that has
+// completed on the device (no sync here; callers check after their step's own synchronisation).
 int peer_ar_error(void* hv) {
   auto* h = static_cast<par::Handle*>(hv);
+  if (h->err_host) return *reinterpret_cast<volatile int*>(h->err_host);
   int v = 0;
   if (hipMemcpy(&v, h->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return v;
+}
+
+// Host-side test hook: a lost peer injected without a GPU fault (tests only).
+void peer_ar_set_error(void* hv, int v) {
+  auto* h = static_cast<par::Handle*>(hv);
+  if (h->err_host) *reinterpret_cast<volatile int*>(h->err_host) = v;
+  else (void)hipMemcpy(h->err, &v, sizeof(int), hipMemcpyHostToDevice);
 }
 
 void peer_ar_destroy(void* hv) {
@@ -448,7 +508,8 @@ void peer_ar_destroy(void* hv) {
     if (h->opened[r]) (void)hipIpcCloseMemHandle(h->peer_base[r]);
   if (h->base) (void)hipFree(h->base);
   if (h->ctr) (void)hipFree(h->ctr);
-  if (h->err) (void)hipFree(h->err);
+  if (h->err_host) (void)hipHostFree(h->err_host);
+  else if (h->err) (void)hipFree(h->err);
   delete h;
 }
 

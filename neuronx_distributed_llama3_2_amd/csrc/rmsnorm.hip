@@ -169,49 +169,68 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ p
   }
 }
 
-// ---- row-per-wave kernels (H a multiple of 512, H <= 4096: every Llama width up to 8B) ---------
-// One wave owns one row at a time: lane l holds the 16-byte vectors l, l+64, ... (VPL = H / 512 of
-// them, each wave-instruction one contiguous KiB), so the row's sum of squares / dot product is a
-// wave reduction with no barrier, and a wave's next row is independent of its neighbours'.  The
+// ---- row-per-wave kernels (H a multiple of 512, H <= 8192: every Llama width to 70B) ----------
+// One wave owns one row (SPLIT = 1, H <= 4096) or one half of it (SPLIT = 2, H 4608 .. 8192: the
+// 70B hidden size); lane l holds the 16-byte vectors l, l+64, ... of its slice (VPL = H / 512 / SPLIT
+// of them, each wave-instruction one contiguous KiB), so a row's sum of squares / dot product is a
+// wave reduction (plus, at SPLIT = 2, one LDS exchange between the two waves of the row and one
+// workgroup barrier per row step) and the register footprint stays that of a 4096-wide row.  The
 // one-row-per-workgroup kernels above paid two block barriers per row and kept little in flight:
 // the backward measured 1.98 TB/s at 8192 x 4096 (profiles/r4_rmsnorm_bwd_pipe_ab.txt), and its
 // 128-workgroup column sum of 512 per-workgroup partials was latency-bound beside concurrent work.
-template <int VPL, bool RES>
+template <int VPL, bool RES, int SPLIT>
 __global__ void __launch_bounds__(256) fwd_rows_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                                                        uint16_t* __restrict__ h_out, float* __restrict__ rstd_out,
                                                        int64_t rows, int H, float eps) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wstride = (int64_t)gridDim.x * 4;
+  constexpr int RPW = 4 / SPLIT;   // rows per workgroup step
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int part = wave % SPLIT, slot = wave / SPLIT;
+  const int col0 = part * VPL * 512 + lane * 8;
   u32x4_t wv[VPL];
 #pragma unroll
-  for (int i = 0; i < VPL; ++i) wv[i] = *reinterpret_cast<const u32x4_t*>(w + (i * 64 + lane) * 8);
-  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += wstride) {
-    const uint16_t* xr = x + row * H + lane * 8;
+  for (int i = 0; i < VPL; ++i) wv[i] = *reinterpret_cast<const u32x4_t*>(w + col0 + i * 512);
+  int step = 0;
+  // the loop bound is workgroup-uniform (every wave reaches every barrier); rows past the end idle
+  for (int64_t base = (int64_t)blockIdx.x * RPW; base < rows; base += (int64_t)gridDim.x * RPW, ++step) {
+    const int64_t row = base + slot;
+    const bool valid = row < rows;
+    const int64_t off = row * H + col0;
     u32x4_t xv[VPL], rv[VPL];
-#pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      xv[i] = *reinterpret_cast<const u32x4_t*>(xr + i * 512);
-      if (RES) rv[i] = *reinterpret_cast<const u32x4_t*>(res + row * H + lane * 8 + i * 512);
-    }
     float ss = 0.f;
+    if (valid) {
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      float v[8];
-      unpack8(xv[i], v);
-      if (RES) {
-        float r[8];
-        unpack8(rv[i], r);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j] + r[j]));   // round like the stored h
-        xv[i] = pack8(v);
-        *reinterpret_cast<u32x4_t*>(h_out + row * H + lane * 8 + i * 512) = xv[i];
+      for (int i = 0; i < VPL; ++i) {
+        xv[i] = *reinterpret_cast<const u32x4_t*>(x + off + i * 512);
+        if (RES) rv[i] = *reinterpret_cast<const u32x4_t*>(res + off + i * 512);
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+      for (int i = 0; i < VPL; ++i) {
+        float v[8];
+        unpack8(xv[i], v);
+        if (RES) {
+          float r[8];
+          unpack8(rv[i], r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j] + r[j]));   // round like the stored h
+          xv[i] = pack8(v);
+          *reinterpret_cast<u32x4_t*>(h_out + off + i * 512) = xv[i];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+      }
     }
-    const float rstd = rsqrtf(wave_sum(ss) / (float)H + eps);
-    if (lane == 0 && rstd_out) rstd_out[row] = rstd;
+    ss = wave_sum(ss);
+    if constexpr (SPLIT > 1) {
+      // the row's two halves meet in LDS (double-buffered by step parity: one barrier per step)
+      if (lane == 0) red[step & 1][wave] = ss;
+      __syncthreads();
+      ss = red[step & 1][slot * SPLIT] + red[step & 1][slot * SPLIT + 1];
+    }
+    if (!valid) continue;
+    const float rstd = rsqrtf(ss / (float)H + eps);
+    if (lane == 0 && part == 0 && rstd_out) rstd_out[row] = rstd;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       float v[8], g[8];
@@ -219,56 +238,71 @@ __global__ void __launch_bounds__(256) fwd_rows_kernel(const uint16_t* __restric
       unpack8(wv[i], g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = v[j] * rstd * g[j];
-      *reinterpret_cast<u32x4_t*>(y + row * H + lane * 8 + i * 512) = pack8(v);
+      *reinterpret_cast<u32x4_t*>(y + off + i * 512) = pack8(v);
     }
   }
 }
 
 // 8 waves per workgroup, one workgroup per CU (G <= 256 workgroups, grid-stride over rows); each lane
-// accumulates dw for its 8 * VPL columns in registers over all of its wave's rows; the 8 waves' sums
+// accumulates dw for its 8 * VPL columns in registers over all of its wave's rows; the waves' sums
 // are added through LDS (fixed order) into ONE partial row per workgroup, so the column sum reads
 // G <= 256 rows instead of 512.  Bitwise reproducible (no atomics, fixed row -> wave assignment).
-template <int VPL, bool RES>
+template <int VPL, bool RES, int SPLIT>
 __global__ void __launch_bounds__(512) bwd_rows_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ h,
                                                        const uint16_t* __restrict__ w, const float* __restrict__ rstd,
                                                        const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
                                                        float* __restrict__ dw_part, int64_t rows, int H) {
+  constexpr int RPW = 8 / SPLIT;
   __shared__ float red[8][520];   // one 512-column slice of the 8 waves' dw sums (+8 pad)
+  __shared__ float dred[2][8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t wstride = (int64_t)gridDim.x * 8;
+  const int part = wave % SPLIT, slot = wave / SPLIT;
+  const int col0 = part * VPL * 512 + lane * 8;
   u32x4_t wv[VPL];
   float dwa[VPL][8];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
-    wv[i] = *reinterpret_cast<const u32x4_t*>(w + (i * 64 + lane) * 8);
+    wv[i] = *reinterpret_cast<const u32x4_t*>(w + col0 + i * 512);
 #pragma unroll
     for (int j = 0; j < 8; ++j) dwa[i][j] = 0.f;
   }
-  for (int64_t row = (int64_t)blockIdx.x * 8 + wave; row < rows; row += wstride) {
-    const int64_t off = row * H + lane * 8;
+  int step = 0;
+  for (int64_t base = (int64_t)blockIdx.x * RPW; base < rows; base += (int64_t)gridDim.x * RPW, ++step) {
+    const int64_t row = base + slot;
+    const bool valid = row < rows;
+    const int64_t off = row * H + col0;
     u32x4_t hv[VPL], dv[VPL], rv[VPL];
+    float rs = 0.f, dot = 0.f;
+    if (valid) {
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      hv[i] = *reinterpret_cast<const u32x4_t*>(h + off + i * 512);
-      dv[i] = *reinterpret_cast<const u32x4_t*>(dy + off + i * 512);
-      if (RES) rv[i] = *reinterpret_cast<const u32x4_t*>(dres + off + i * 512);
-    }
-    const float rs = rstd[row];
-    float dot = 0.f;
+      for (int i = 0; i < VPL; ++i) {
+        hv[i] = *reinterpret_cast<const u32x4_t*>(h + off + i * 512);
+        dv[i] = *reinterpret_cast<const u32x4_t*>(dy + off + i * 512);
+        if (RES) rv[i] = *reinterpret_cast<const u32x4_t*>(dres + off + i * 512);
+      }
+      rs = rstd[row];
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      float a[8], d[8], g[8];
-      unpack8(hv[i], a);
-      unpack8(dv[i], d);
-      unpack8(wv[i], g);
+      for (int i = 0; i < VPL; ++i) {
+        float a[8], d[8], g[8];
+        unpack8(hv[i], a);
+        unpack8(dv[i], d);
+        unpack8(wv[i], g);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = a[j] * rs;
-        dot += d[j] * g[j] * xh;
-        dwa[i][j] += d[j] * xh;
+        for (int j = 0; j < 8; ++j) {
+          const float xh = a[j] * rs;
+          dot += d[j] * g[j] * xh;
+          dwa[i][j] += d[j] * xh;
+        }
       }
     }
-    const float mean = wave_sum(dot) / (float)H;
+    dot = wave_sum(dot);
+    if constexpr (SPLIT > 1) {
+      if (lane == 0) dred[step & 1][wave] = dot;
+      __syncthreads();
+      dot = dred[step & 1][slot * SPLIT] + dred[step & 1][slot * SPLIT + 1];
+    }
+    if (!valid) continue;
+    const float mean = dot / (float)H;
     // re-unpack from the packed registers below instead of keeping the first pass's 3 x 8 x VPL
     // unpacked floats alive (at VPL = 8 that spilled ~100 VGPRs)
 #pragma unroll
@@ -290,7 +324,8 @@ __global__ void __launch_bounds__(512) bwd_rows_kernel(const uint16_t* __restric
       *reinterpret_cast<u32x4_t*>(dx + off + i * 512) = pack8(o);
     }
   }
-  // workgroup partial: slice i (columns [512 i, 512 i + 512)) of the 8 waves' sums, in wave order
+  // workgroup partial: slice i (columns [512 i, 512 i + 512) of each wave's part) of the waves' sums,
+  // the waves of one part added in wave order
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     __syncthreads();
@@ -298,10 +333,13 @@ __global__ void __launch_bounds__(512) bwd_rows_kernel(const uint16_t* __restric
     for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = dwa[i][j];
     __syncthreads();
     const int c = threadIdx.x;   // 512 threads = the slice's 512 columns
-    float t = 0.f;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) t += red[q][c];
-    dw_part[(int64_t)blockIdx.x * H + i * 512 + c] = t;
+    for (int pp = 0; pp < SPLIT; ++pp) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = pp; q < 8; q += SPLIT) t += red[q][c];
+      dw_part[(int64_t)blockIdx.x * H + pp * VPL * 512 + i * 512 + c] = t;
+    }
   }
 }
 
@@ -336,7 +374,7 @@ static bool rows_path(int H) {
     const char* e = getenv("NXD_RMS_ROWS");
     g_rows_mode = e ? (atoi(e) != 0) : 1;
   }
-  return g_rows_mode && H % 512 == 0 && H >= 512 && H <= 4096;
+  return g_rows_mode && H % 512 == 0 && H >= 512 && H <= 8192 && (H <= 4096 || H % 1024 == 0);
 }
 
 }  // namespace rms
@@ -347,25 +385,29 @@ int rmsnorm_fwd_launch(const void* x, const void* res, const void* w, void* y, v
   if (H % 8 != 0) return -1;
   if (rows_path(H)) {
     if (rows == 0) return 0;
-    const int g = (int)std::min<int64_t>(ceil_div64(rows, 4), 2048);
-#define RMS_FWD_ROWS(V)                                                                                        \
+    const int g = (int)std::min<int64_t>(ceil_div64(rows, H <= 4096 ? 4 : 2), 2048);
+#define RMS_FWD_ROWS(V, S)                                                                                     \
   do {                                                                                                         \
     if (res)                                                                                                   \
-      hipLaunchKernelGGL((fwd_rows_kernel<V, true>), dim3(g), dim3(256), 0, stream, (const uint16_t*)x,         \
+      hipLaunchKernelGGL((fwd_rows_kernel<V, true, S>), dim3(g), dim3(256), 0, stream, (const uint16_t*)x,      \
                          (const uint16_t*)res, (const uint16_t*)w, (uint16_t*)y, (uint16_t*)h_out, rstd, rows, H, eps); \
     else                                                                                                       \
-      hipLaunchKernelGGL((fwd_rows_kernel<V, false>), dim3(g), dim3(256), 0, stream, (const uint16_t*)x,        \
+      hipLaunchKernelGGL((fwd_rows_kernel<V, false, S>), dim3(g), dim3(256), 0, stream, (const uint16_t*)x,     \
                          (const uint16_t*)res, (const uint16_t*)w, (uint16_t*)y, (uint16_t*)h_out, rstd, rows, H, eps); \
   } while (0)
     switch (H / 512) {
-      case 1: RMS_FWD_ROWS(1); break;
-      case 2: RMS_FWD_ROWS(2); break;
-      case 3: RMS_FWD_ROWS(3); break;
-      case 4: RMS_FWD_ROWS(4); break;
-      case 5: RMS_FWD_ROWS(5); break;
-      case 6: RMS_FWD_ROWS(6); break;
-      case 7: RMS_FWD_ROWS(7); break;
-      default: RMS_FWD_ROWS(8); break;
+      case 1: RMS_FWD_ROWS(1, 1); break;
+      case 2: RMS_FWD_ROWS(2, 1); break;
+      case 3: RMS_FWD_ROWS(3, 1); break;
+      case 4: RMS_FWD_ROWS(4, 1); break;
+      case 5: RMS_FWD_ROWS(5, 1); break;
+      case 6: RMS_FWD_ROWS(6, 1); break;
+      case 7: RMS_FWD_ROWS(7, 1); break;
+      case 8: RMS_FWD_ROWS(8, 1); break;
+      case 10: RMS_FWD_ROWS(5, 2); break;
+      case 12: RMS_FWD_ROWS(6, 2); break;
+      case 14: RMS_FWD_ROWS(7, 2); break;
+      default: RMS_FWD_ROWS(8, 2); break;   // 16: H = 8192
     }
 #undef RMS_FWD_ROWS
     return (int)hipGetLastError();
@@ -396,28 +438,32 @@ int rmsnorm_bwd_launch(const void* dy, const void* h, const void* w, const float
   if (H % 8 != 0) return -1;
   if (rows_path(H)) {
     // G <= 256 <= rmsnorm_bwd_num_partials(rows) for rows >= 256 (and ceil(rows / 8) <= rows below)
-    const int G = (int)std::min<int64_t>(ceil_div64(rows, 8), 256);
+    const int G = (int)std::min<int64_t>(ceil_div64(rows, H <= 4096 ? 8 : 4), 256);
     if (G == 0) return 0;
-#define RMS_BWD_ROWS(V)                                                                                        \
+#define RMS_BWD_ROWS(V, S)                                                                                     \
   do {                                                                                                         \
     if (dres)                                                                                                  \
-      hipLaunchKernelGGL((bwd_rows_kernel<V, true>), dim3(G), dim3(512), 0, stream, (const uint16_t*)dy,        \
+      hipLaunchKernelGGL((bwd_rows_kernel<V, true, S>), dim3(G), dim3(512), 0, stream, (const uint16_t*)dy,     \
                          (const uint16_t*)h, (const uint16_t*)w, rstd, (const uint16_t*)dres, (uint16_t*)dx, dw_part, \
                          rows, H);                                                                             \
     else                                                                                                       \
-      hipLaunchKernelGGL((bwd_rows_kernel<V, false>), dim3(G), dim3(512), 0, stream, (const uint16_t*)dy,       \
+      hipLaunchKernelGGL((bwd_rows_kernel<V, false, S>), dim3(G), dim3(512), 0, stream, (const uint16_t*)dy,    \
                          (const uint16_t*)h, (const uint16_t*)w, rstd, (const uint16_t*)dres, (uint16_t*)dx, dw_part, \
                          rows, H);                                                                             \
   } while (0)
     switch (H / 512) {
-      case 1: RMS_BWD_ROWS(1); break;
-      case 2: RMS_BWD_ROWS(2); break;
-      case 3: RMS_BWD_ROWS(3); break;
-      case 4: RMS_BWD_ROWS(4); break;
-      case 5: RMS_BWD_ROWS(5); break;
-      case 6: RMS_BWD_ROWS(6); break;
-      case 7: RMS_BWD_ROWS(7); break;
-      default: RMS_BWD_ROWS(8); break;
+      case 1: RMS_BWD_ROWS(1, 1); break;
+      case 2: RMS_BWD_ROWS(2, 1); break;
+      case 3: RMS_BWD_ROWS(3, 1); break;
+      case 4: RMS_BWD_ROWS(4, 1); break;
+      case 5: RMS_BWD_ROWS(5, 1); break;
+      case 6: RMS_BWD_ROWS(6, 1); break;
+      case 7: RMS_BWD_ROWS(7, 1); break;
+      case 8: RMS_BWD_ROWS(8, 1); break;
+      case 10: RMS_BWD_ROWS(5, 2); break;
+      case 12: RMS_BWD_ROWS(6, 2); break;
+      case 14: RMS_BWD_ROWS(7, 2); break;
+      default: RMS_BWD_ROWS(8, 2); break;   // 16: H = 8192
     }
 #undef RMS_BWD_ROWS
     hipLaunchKernelGGL(colsum4_kernel, dim3((H + 63) / 64), dim3(256), 0, stream, dw_part, dw, G, H, accumulate_dw);

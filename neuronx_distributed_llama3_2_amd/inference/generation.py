@@ -452,6 +452,8 @@ class LlamaForCausalLMInference:
         else:
             gen.seed()
         logits = self._context_encode(input_ids, attention_mask)
+        if hasattr(self.model, "check_collectives"):
+            self.model.check_collectives()
         u0 = torch.rand(B, device=dev, generator=gen)
         first = sampler.sample(logits, u0)
         new = [first.view(B, 1)]
@@ -461,11 +463,17 @@ class LlamaForCausalLMInference:
             uni = torch.rand((st.max_steps, Bp), device=dev, generator=gen)
             st.load(first, lengths, torch.arange(Bp, device=dev), uni)
             g = self._graph(Bp, sampler)
+            st_tp = getattr(self.model, "_tp_dec", None)
+            peer = st_tp is not None and type(st_tp["ar"]).__name__ == "PeerAllReduce"
             todo = max_new_tokens - 1
             done_steps = 0
             while done_steps < todo:
                 g.replay()
                 done_steps += g.steps
+                if peer:
+                    # a lost TP peer wrote NaN logits / residuals: fail this generate(), never emit them
+                    torch.cuda.current_stream().synchronize()
+                    self.model.check_collectives()
                 if eos.numel():
                     seen = torch.isin(torch.cat([first.view(B, 1), st.out[:, :min(done_steps, todo)]], 1), eos)
                     if bool(seen.any(1).all()):

@@ -273,6 +273,13 @@ class DecoderInferenceMixin:
             return False
         return isinstance(self._decode_tp_state(ew.shape[1], ew.device)["ar"], PeerAllReduce)
 
+    def check_collectives(self) -> None:
+        """Raise if the TP decode all-reduce lost a peer since it was built (a pinned host word: the
+        caller synchronises first so its own step is covered)."""
+        st = getattr(self, "_tp_dec", None)
+        if st is not None:
+            st["ar"].check()
+
     def _decode_tp_state(self, H: int, device):
         """TP > 1 fused decode: fp32 [8, H] partial / sum buffers and the decode all-reduce (one-shot
         peer all-reduce over IPC when available -- parallel/peer_allreduce.py -- else the process

@@ -165,6 +165,18 @@ def _peer_for(group, t: torch.Tensor, op=None):
     return c
 
 
+def check_peer_collectives(sync: bool = True) -> None:
+    """Raise if a peer collective lost a peer (csrc/peer_allreduce.hip marks the call and writes NaN):
+    the optimizer step calls this whenever the peer path carried the step's collectives, after a
+    stream sync so the step's own calls are covered (the error word is pinned host memory)."""
+    if not _peer_colls:
+        return
+    if sync and torch.cuda.is_available():
+        torch.cuda.current_stream().synchronize()
+    for c in _peer_colls.values():
+        c.check()
+
+
 def _native_result(work, async_op: bool, op: str, t: torch.Tensor):
     if not async_op:
         return None

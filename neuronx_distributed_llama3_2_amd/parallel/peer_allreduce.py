@@ -65,10 +65,40 @@ class PeerAllReduce:
         if bad:
             self.close()
             raise RuntimeError(f"peer all-reduce unavailable: {bad[0]}")
+        self._failed = None
+        self._calls = 0
+        self._drop = _drop_spec(self.rank)
+        # Before first use: a per-rank pattern through the REAL kernel and the IPC mappings, checked on
+        # every rank.  This is what admits the coarse-grained fallback (no uncached IPC export) for a
+        # group spread over several GPUs: visibility across devices then rests on the system-scope
+        # fences alone, so it must be shown, not assumed.
+        ok = self._self_test()
+        oks = [None] * self.world
+        dist.all_gather_object(oks, ok, group=group)
+        if not all(oks):
+            self.close()
+            raise RuntimeError(f"peer all-reduce self-test failed on rank(s) {[r for r, o in enumerate(oks) if not o]} "
+                               f"(uncached={bool(self.uncached)}); refusing the peer path")
+
+    def _self_test(self) -> bool:
+        n = min(self.nmax, 4096) // 4 * 4
+        i = torch.arange(n, device="cuda", dtype=torch.float32)
+        pat = lambda r: (r + 1) * 1000.0 + (i % 61)   # noqa: E731
+        inp = pat(self.rank)
+        out = torch.empty(n, device="cuda")
+        self.C.peer_ar_run(self.h, inp, False, SUM, out, None, None)
+        torch.cuda.current_stream().synchronize()
+        want = sum(pat(r) for r in range(self.world))
+        return bool(torch.equal(out, want)) and int(self.C.peer_ar_error(self.h)) == 0
 
     def _run(self, inp: torch.Tensor, zero_in: bool, mode: int, out=None, res=None, xadd=None):
         if inp.numel() > self.nmax or inp.numel() % 4:
             raise ValueError(f"peer all-reduce: {inp.numel()} elements (max {self.nmax}, multiple of 4)")
+        if self._failed:
+            raise RuntimeError(self._failed)
+        self._calls += 1
+        if self._drop is not None and self._calls == self._drop:
+            return   # test hook (NXD_PEER_AR_DROP): this rank skips one call -- its peers must notice
         self.C.peer_ar_run(self.h, inp, zero_in, mode, out, res, xadd)
 
     def sum_(self, inp: torch.Tensor, out: torch.Tensor, zero_in: bool = False) -> torch.Tensor:
@@ -92,8 +122,19 @@ class PeerAllReduce:
         return out
 
     def error_count(self) -> int:
-        """Calls in which some peer never arrived within the bounded spin (0 when healthy)."""
-        return int(self.C.peer_ar_error(self.h))
+        """Non-zero once some call lost a peer (bounded spin expired, or the peers' call sequences
+        diverged).  A pinned host word: free to read, covers every call that has completed on the GPU."""
+        return int(self.C.peer_ar_error(self.h)) if self.h else 0
+
+    def check(self) -> None:
+        """Raise if any completed call lost a peer.  Such a call wrote NaN outputs and the ranks' epochs
+        no longer agree, so the handle stays failed: every later call raises too."""
+        if self._failed:
+            raise RuntimeError(self._failed)
+        if self.error_count():
+            self._failed = (f"peer all-reduce: a peer of rank {self.rank} never arrived or skipped a call (world "
+                            f"{self.world}); the results of this step are invalid (NaN) and the group is unusable")
+            raise RuntimeError(self._failed)
 
     def close(self) -> None:
         if getattr(self, "h", None):
@@ -144,8 +185,23 @@ class ProcessGroupAllReduce:
     def error_count(self) -> int:
         return 0
 
+    def check(self) -> None:
+        pass
+
     def close(self) -> None:
         pass
+
+
+def _drop_spec(rank: int):
+    """NXD_PEER_AR_DROP="r:k": rank r silently skips its k-th peer all-reduce call (the error-path
+    tests inject a lost peer with it)."""
+    import os
+
+    spec = os.environ.get("NXD_PEER_AR_DROP", "")
+    if not spec:
+        return None
+    r, k = spec.split(":")
+    return int(k) if int(r) == rank else None
 
 
 def make_decode_all_reduce(group, nmax: int, device: Optional[torch.device] = None, prefer_peer: bool = True):
@@ -193,10 +249,20 @@ class PeerCollectives:
 
     def _ensure(self, nbytes: int) -> PeerAllReduce:
         if self.par is None or nbytes > self.cap:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("peer collectives: the region must be sized before graph capture "
+                                   f"({nbytes} B requested, {self.cap} B mapped)")
+            # every rank grows at the same call (same shapes everywhere); agree on the largest request
+            # so no rank maps a smaller region than a peer will write
+            probe = torch.tensor([int(nbytes)], dtype=torch.int64,
+                                 device="cuda" if dist.get_backend(self.group) == "nccl" else "cpu")
+            dist.all_reduce(probe, op=dist.ReduceOp.MAX, group=self.group)
+            nbytes = int(probe.item())
             cap = max(1 << 20, 1 << (int(nbytes) - 1).bit_length())
             if self.par is not None:
                 torch.cuda.synchronize()
                 dist.barrier(group=self.group)
+                self.par.check()
                 self.par.close()
             self.par = PeerAllReduce(self.group, nmax=cap // 4)
             self.cap = cap
@@ -227,3 +293,7 @@ class PeerCollectives:
 
     def error_count(self) -> int:
         return self.par.error_count() if self.par is not None else 0
+
+    def check(self) -> None:
+        if self.par is not None:
+            self.par.check()

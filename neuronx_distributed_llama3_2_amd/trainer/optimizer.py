@@ -16,6 +16,7 @@ from typing import Any, Dict
 
 import torch
 
+from ..parallel import comm
 from ..parallel_layers import parallel_state, stream_split
 from ..parallel_layers.grads import allreduce_sequence_parallel_gradients, bucket_allreduce_gradients, clip_grad_norm
 
@@ -72,6 +73,7 @@ class NxDOptimizer(torch.optim.Optimizer):
         # the two sequence-parallel halves' streams (parallel_layers/stream_split.py) end the
         # backward and write main_grad: every optimizer kind reads gradients after them
         stream_split.join()
+        comm.check_peer_collectives()   # a lost peer (NXD_SP_PEER) raises before its NaN grads are applied
         if self._flat:
             return self.optimizer.step(closure)
         params = self._params()

@@ -586,10 +586,11 @@ def test_adamw_stochastic_rounding_matches_reference():
     assert abs(err) < 1e-4, err
 
 
-@pytest.mark.parametrize("H", [512, 1536, 3072, 4096])
+@pytest.mark.parametrize("H", [512, 1536, 3072, 4096, 6144, 8192])
 @pytest.mark.parametrize("T", [1, 9, 2049, 5003])
 def test_rmsnorm_rows_path_vs_fp32(H, T):
-    """Row-per-wave RMSNorm kernels (H % 512 == 0, H <= 4096; csrc/rmsnorm.hip fwd_rows / bwd_rows /
+    """Row-per-wave RMSNorm kernels (H % 512 == 0, H <= 8192 -- two waves per row above 4096, the 70B
+    width; csrc/rmsnorm.hip fwd_rows / bwd_rows /
     colsum4): rows below and above the grid's 8 x 256 rows per round (grid-stride), residual fused,
     dw accumulated into a nonzero fp32 main_grad -- against fp32 torch, and against the one-row-per-
     workgroup kernels."""
