@@ -407,6 +407,201 @@ __global__ void __launch_bounds__(NT, 1) gemm_kernel(Params p) {
   }
 }
 
+// ---- PIPE 2: four waves of 128 x 128 (one per SIMD) on v_mfma_f32_32x32x16_bf16 ------------------
+// The 8-wave kernel above spends ~30 % of its wave-cycles parked at barriers and fragment waits
+// (MFMA busy 57 % at 8192 x 4096 x 4096, SQ_WAIT_ANY 0.315 of wave cycles: profiles/r6_dense_gemm_pmc.txt).
+// Here each wave owns a 128 x 128 quarter of the tile -- 4 x 4 32x32 accumulator tiles, 256 registers
+// (a lone wave per SIMD has 512) -- and reads 8 fragments per 16 MFMAs of 32 cycles, each k-step's
+// fragments read into the other register set while the current one feeds the MFMAs:
+//   tile t, k-steps 0..3 (16 k each):  reads (t, ks+1) -> other set | 16 MFMAs on this set
+//   after k-step 2: lgkmcnt(0) + vmcnt(0) (this thread's pieces of tile t+1) + ONE barrier; k-step 3
+//   reads (t+1, 0) and issues the LDS-DMA of tile t+2 into tile t's buffer (all its reads retired)
+// so a tile's DMA has four k-steps (~2,000 cycles) to land.  (The 16x16x32 form of this structure
+// made hipcc shuttle the 64 four-register accumulators between AGPRs and VGPRs every iteration.)
+// LDS images as above except the TN swizzle: 256-B rows with chunk c of row t at
+// c ^ (((t & 3) << 2) | ((t >> 2) & 3)) (cdna_hip_programming.md T10 (b)), under which the 32-lane
+// halves of the 32x32x16 transposed operand reads are conflict-free.
+constexpr int NT4 = 256;
+
+__device__ __forceinline__ int tn4_swz(int t) { return ((t & 3) << 2) | ((t >> 2) & 3); }
+
+// 32x32x16 operand of region rows / features [x0, x0 + 32), k-step ks (16 k): lane l -> row / feature
+// x0 + (l & 31), k = 16 ks + 8 (l >> 5) + j
+template <int L>
+__device__ __forceinline__ bf16x8_t frag32(const char* reg, int x0, int ks) {
+  const int l = threadIdx.x & 63;
+  if constexpr (L == LNT) {
+    const int r = x0 + (l & 31), ch = 2 * ks + (l >> 5);
+    return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u32x4_t*>(reg + r * 128 + ((ch ^ nt_swz(r)) << 4)));
+  } else {
+    const int g = l >> 4, q = (l >> 2) & 3, pp = l & 3;
+    const int t = 16 * ks + 8 * (g >> 1) + q;
+    const int ch = (x0 >> 3) + 2 * (g & 1) + (pp >> 1);
+    const char* b0 = reg + t * 256 + ((ch ^ tn4_swz(t)) << 4) + 8 * (pp & 1);
+    const char* b1 = reg + (t + 4) * 256 + ((ch ^ tn4_swz(t + 4)) << 4) + 8 * (pp & 1);
+    const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)b0);
+    const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)b1);
+    const short __attribute__((ext_vector_type(8))) a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, a8);
+  }
+}
+
+template <int L, int E>
+__global__ void __launch_bounds__(NT4, 1) gemm4_kernel(Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  const int tiles = p.mt * p.nt;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = id / tiles;
+  int rt, ct;
+  {
+    const int within = id - split * tiles;
+    const int kb = p.band, bnd = within / (kb * p.nt), rem = within - bnd * kb * p.nt;
+    const int h = min(kb, p.mt - bnd * kb);
+    rt = bnd * kb + rem % h;
+    ct = rem / h;
+  }
+  const int m0 = rt * BM, n0 = ct * BN;
+  const int k_begin = split * p.k_per_split;
+  const int k_end = min(p.K, k_begin + p.k_per_split);
+  const int nk = (k_end - k_begin) / BK;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wid >> 1, wc = wid & 1;
+
+  f32x16_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // Per-lane DMA sources of K-tile 0.  Full tiles only (M, N % 256 == 0: the launcher checks), so the
+  // 4 pieces x 2 halves of one operand differ by uniform row / token offsets, except for the source
+  // swizzle: NT's depends on the piece's parity (2 pointers per operand), TN's on the piece (4).
+  constexpr int NV = L == LNT ? 2 : 4;
+  const uint16_t* sa[NV];
+  const uint16_t* sb[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    if constexpr (L == LNT) {
+      const int pr = 8 * (4 * wid + v) + (lane >> 3), c = (lane & 7) ^ nt_swz(pr);
+      sa[v] = p.a + (int64_t)(m0 + pr) * p.lda + k_begin + 8 * c;
+      sb[v] = p.b + (int64_t)(n0 + pr) * p.ldb + k_begin + 8 * c;
+    } else {
+      const int pr = 4 * (4 * wid + v) + (lane >> 4), c = (lane & 15) ^ tn4_swz(pr);
+      sa[v] = p.a + (int64_t)(k_begin + pr) * p.lda + m0 + 8 * c;
+      sb[v] = p.b + (int64_t)(k_begin + pr) * p.ldb + n0 + 8 * c;
+    }
+  }
+  auto pv = [](int j) { return L == LNT ? (j & 1) : j; };
+  auto poff = [&](int h, int j, int64_t ld) -> int64_t {
+    if constexpr (L == LNT) return (int64_t)(128 * h + 8 * (j & ~1)) * ld;
+    else return (int64_t)128 * h;
+  };
+  const int64_t adv_a = L == LNT ? (int64_t)BK : (int64_t)BK * p.lda;
+  const int64_t adv_b = L == LNT ? (int64_t)BK : (int64_t)BK * p.ldb;
+  const uint32_t lds0 = lds_addr(smem);
+  // piece q (0..15) of K-tile s: region q / 4 (A_lo, A_hi, B_lo, B_hi), piece j = q % 4
+  auto issue_piece = [&](int s, int q) {
+    const int r = q >> 2, j = q & 3, h = r & 1;
+    const uint32_t dst = lds0 + (s & 1) * BUF + (r == 0 ? R_ALO : r == 1 ? R_AHI : r == 2 ? R_BLO : R_BHI) + wid * 4096 + j * 1024;
+    const uint16_t* src = r < 2 ? sa[pv(j)] + (int64_t)s * adv_a + poff(h, j, p.lda)
+                                : sb[pv(j)] + (int64_t)s * adv_b + poff(h, j, p.ldb);
+    dma16(src, __builtin_amdgcn_readfirstlane(dst));
+  };
+  const int ra = wr ? R_AHI : R_ALO, rb = wc ? R_BHI : R_BLO;
+  bf16x8_t fa0[4], fb0[4], fa1[4], fb1[4];
+  auto rd = [&](const char* buf, int ks, bf16x8_t (&fa)[4], bf16x8_t (&fb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = frag32<L>(buf + ra, 32 * i, ks);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = frag32<L>(buf + rb, 32 * j, ks);
+  };
+  auto mm = [&](bf16x8_t (&fa)[4], bf16x8_t (&fb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  };
+
+#pragma unroll
+  for (int q = 0; q < 16; ++q) issue_piece(0, q);
+  if (nk > 1) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) issue_piece(1, q);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier();
+  rd(smem, 0, fa0, fb0);
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+    rd(buf, 1, fa1, fb1);
+    mm(fa0, fb0);
+    rd(buf, 2, fa0, fb0);
+    mm(fa1, fb1);
+    rd(buf, 3, fa1, fb1);
+    mm(fa0, fb0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's pieces of tile t+1
+    barrier();
+    rd(smem + ((t + 1) & 1) * BUF, 0, fa0, fb0);      // past the last tile: stale LDS, never consumed
+    if (t + 2 < nk) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) issue_piece(t + 2, q);
+    }
+    mm(fa1, fb1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: per wave 4 passes of 32 rows x 128 columns through a padded fp32 LDS slab
+  constexpr int LD = 132;
+  float* slab = reinterpret_cast<float*>(smem) + wid * (32 * LD);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        slab[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * LD + 32 * j + (lane & 31)] = acc[i][j][r];
+    __builtin_amdgcn_wave_barrier();
+    const int row0 = m0 + 128 * wr + 32 * i, col0 = n0 + 128 * wc;
+    if constexpr (E == F32_ATOMIC) {
+      float* cp = static_cast<float*>(p.c);
+#pragma unroll 2
+      for (int rr = 0; rr < 64; ++rr) {   // half a row (256 contiguous bytes) per wave-instruction
+        const int lr = rr >> 1, col = col0 + 64 * (rr & 1) + lane, row = row0 + lr;
+        const float v = slab[lr * LD + 64 * (rr & 1) + lane];
+        if (row < p.M && col < p.N) unsafeAtomicAdd(cp + (int64_t)row * p.ldc + col, v);
+      }
+    } else {
+#pragma unroll
+      for (int ps = 0; ps < 8; ++ps) {   // 16 lanes x 8 columns per row, 4 rows per pass
+        const int lr = 4 * ps + (lane >> 4), c8 = 8 * (lane & 15);
+        const int row = row0 + lr, col = col0 + c8;
+        const f32x4_t v0 = *reinterpret_cast<const f32x4_t*>(slab + lr * LD + c8);
+        const f32x4_t v1 = *reinterpret_cast<const f32x4_t*>(slab + lr * LD + c8 + 4);
+        if (row < p.M && col < p.N) {
+          if constexpr (E == BF16) {
+            u32x4_t o;
+            o[0] = pack2bf(v0[0], v0[1]); o[1] = pack2bf(v0[2], v0[3]);
+            o[2] = pack2bf(v1[0], v1[1]); o[3] = pack2bf(v1[2], v1[3]);
+            *reinterpret_cast<u32x4_t*>(static_cast<uint16_t*>(p.c) + (int64_t)row * p.ldc + col) = o;
+          } else {
+            f32x4_t* cp = reinterpret_cast<f32x4_t*>(static_cast<float*>(p.c) + (int64_t)row * p.ldc + col);
+            const f32x4_t c0 = cp[0], c1 = cp[1];
+            cp[0] = c0 + v0;
+            cp[1] = c1 + v1;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 static int g_pipe = -1;   // main-loop variant override (dense_gemm_set_pipe, in-process A/B)
 
 static int env_int(const char* name, int dflt) {
@@ -464,11 +659,15 @@ int dense_gemm_launch(int layout, int epi, const void* a, int64_t lda, const voi
   p.band = band;
   const int64_t nwg = (int64_t)p.mt * p.nt * p.splits;
   if (nwg > INT32_MAX) return -2;
+  // default: the 8-wave register-pipelined loop (PIPE 1), the fastest of the three on every measured
+  // shape (profiles/r6_dense_gemm_pipes_vs_hipblaslt.jsonl: PIPE 2 5-20 % slower, PIPE 0 2-9 %)
   static int pipe_env = dg::env_int("NXD_DG_PIPE", 1);
-  const int pipe = dg::g_pipe >= 0 ? dg::g_pipe : pipe_env;
+  int pipe = dg::g_pipe >= 0 ? dg::g_pipe : pipe_env;
+  if (pipe == 2 && (M % dg::BM || N % dg::BN)) pipe = 1;   // the 4-wave kernel takes whole tiles only
 #define NXD_DG_LAUNCH(LY, EP)                                                                                  \
   do {                                                                                                       \
-    if (pipe) hipLaunchKernelGGL((dg::gemm_kernel<LY, EP, 1>), dim3((unsigned)nwg), dim3(dg::NT), 0, stream, p); \
+    if (pipe == 2) hipLaunchKernelGGL((dg::gemm4_kernel<LY, EP>), dim3((unsigned)nwg), dim3(dg::NT4), 0, stream, p); \
+    else if (pipe) hipLaunchKernelGGL((dg::gemm_kernel<LY, EP, 1>), dim3((unsigned)nwg), dim3(dg::NT), 0, stream, p); \
     else hipLaunchKernelGGL((dg::gemm_kernel<LY, EP, 0>), dim3((unsigned)nwg), dim3(dg::NT), 0, stream, p);      \
   } while (0)
   if (layout == dg::LNT) {

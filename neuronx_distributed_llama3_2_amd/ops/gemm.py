@@ -117,6 +117,40 @@ def _use_wgrad_kernel(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor, has
     return _WG_KERNEL == "1" or M * N / (M + N) < _WG_SKINNY or (not has_copy and max(M, N) >= _WG_WIDE)
 
 
+# The hand-written dense GEMM (csrc/dense_gemm.hip) in its TN form reads the token-major dy / x
+# directly (no transposes) and adds into the fp32 main_grad: one read-modify-write per element when
+# a single K split fills the chip, split-K float atomics otherwise.  Measured against this module's
+# other routes at the Llama-3-8B shapes (profiles/r6_dense_gemm_pipes_vs_hipblaslt.jsonl, T = 8192 /
+# 65536): it wins every TP=8 shard -- qkv 1018 vs 880 TF/s, o_proj 1005 vs 904, gate_up 1180 vs 1164,
+# down 1073 vs 961 -- and the TP=1 o_proj (1236 vs 1092, whose hipBLASLt route transposes both
+# operands), and loses the wide TP=1 shapes to hipBLASLt's TN GEMM on producer-written copies
+# (qkv 955 vs 1070, gate_up 1130 vs 1195, down 1063 vs 1152).  Rule: no producer copy, and
+# M N / (M + N) < 2200.  NXD_DENSE_WGRAD = auto | 1 (whenever the shapes allow) | 0.
+_DENSE_WG = os.environ.get("NXD_DENSE_WGRAD", "auto")
+_DENSE_WG_SKINNY = 2200.0
+
+
+def _use_dense_wgrad(mg: torch.Tensor, go2: torch.Tensor, x2, has_copy: bool) -> bool:
+    if _DENSE_WG == "0" or x2 is None or not _native(go2, x2) or mg.dtype != torch.float32:
+        return False
+    T, M = go2.shape
+    N = x2.shape[1]
+    if T % 64 or M % 8 or N % 8 or go2.stride(1) != 1 or x2.stride(1) != 1 or mg.stride(1) != 1:
+        return False
+    if go2.stride(0) % 8 or x2.stride(0) % 8 or mg.stride(0) % 4:
+        return False
+    if go2.data_ptr() % 16 or x2.data_ptr() % 16 or mg.data_ptr() % 16:
+        return False
+    return _DENSE_WG == "1" or (not has_copy and M * N / (M + N) < _DENSE_WG_SKINNY)
+
+
+def _dense_wgrad(mg: torch.Tensor, go2: torch.Tensor, x2: torch.Tensor) -> None:
+    C = ext()
+    T, M = go2.shape
+    splits = C.dense_gemm_splits(M, x2.shape[1], T)
+    C.dense_gemm(1, 1 if splits == 1 else 2, go2, x2, mg, splits)
+
+
 def _wgrad_scratch(n: int, dtype, device, tag: str = "") -> torch.Tensor:
     # one buffer per stream: the two halves of parallel_layers/stream_split.py transpose concurrently
     sid = torch.cuda.current_stream(device).stream_id if torch.device(device).type == "cuda" else 0
@@ -139,7 +173,11 @@ def wgrad_accumulate_(mg: torch.Tensor, go2: torch.Tensor, x2, go_t: torch.Tenso
     into a reused scratch, then an fp32 add (the per-micro-batch weight gradient is rounded to
     bf16 before the fp32 accumulation — the precision of the reference's XLA matmul + fp32
     grad accumulation; hipBLASLt's bf16-output solutions run faster than its fp32-output ones)."""
-    if _use_wgrad_kernel(mg, go2, x2, has_copy=go_t is not None or x_t is not None):
+    has_copy = go_t is not None or x_t is not None
+    if _use_dense_wgrad(mg, go2, x2, has_copy):
+        _dense_wgrad(mg, go2, x2)
+        return
+    if _use_wgrad_kernel(mg, go2, x2, has_copy=has_copy):
         ext().wgrad_gemm(mg, go2, x2, 0)
         return
     if x_t is not None and not (x_t.dim() == 2 and x_t.is_contiguous() and x_t.shape[1] == go2.shape[0]):

@@ -67,3 +67,24 @@ def test_dense_gemm_rejects_bad_shapes():
     c = torch.empty(64, 64, device="cuda", dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         ext().dense_gemm(0, 0, a, b, c)   # K % 64 != 0
+
+
+def test_framework_wgrad_routes_skinny_shards_to_dense_tn():
+    """ops.gemm.wgrad_accumulate_ sends the tensor-parallel shards and the TP=1 o_proj (no producer copy,
+    M N / (M + N) < 2200) to the hand-written TN kernel -- RMW epilogue when one K split fills the chip,
+    split-K atomics otherwise -- and keeps hipBLASLt for the wide TP=1 shapes; all accumulate like fp64."""
+    from neuronx_distributed_llama3_2_amd.ops import gemm as G
+
+    torch.manual_seed(3)
+    for (T, M, N, copy, want) in [(512, 768, 4096, False, True), (1024, 4096, 512, False, True),
+                                  (512, 4096, 4096, False, True), (512, 6144, 4096, False, False),
+                                  (512, 768, 4096, True, False), (288, 768, 4096, False, False)]:
+        dy = torch.randn(T, M, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+        mg = torch.randn(M, N, device="cuda", dtype=torch.float32)
+        go_t = dy.t().contiguous() if copy else None
+        assert G._use_dense_wgrad(mg, dy, x, has_copy=copy) == (want and G._DENSE_WG != "0"), (T, M, N, copy)
+        ref = mg.double() + dy.double().t() @ x.double()
+        G.wgrad_accumulate_(mg, dy, x, go_t=go_t)
+        scale = dy.double().abs().t() @ x.double().abs()
+        assert torch.all((mg.double() - ref).abs() <= 1e-5 * scale + 1e-4)
