@@ -22,7 +22,9 @@
 //   2. publishes: every wave drains its stores (vmcnt(0)), workgroup barrier, one system-scope release
 //      (the region may be read from another GPU over xGMI), then the flag[parity][b] = e store;
 //   3. waits for flag[parity][b] >= e of every peer (relaxed system-scope polls with s_sleep and a
-//      bounded spin), then one system-scope acquire and a barrier.  A peer that never arrives, or whose
+//      bounded spin; the flag word also carries the call's signature, so peers whose call sequences
+//      drifted apart are told from peers that are merely late), then one system-scope acquire and a
+//      barrier.  A peer that never arrives, or whose
 //      flag is PAST e (it skipped a call: the two ranks' call sequences diverged), marks the call
 //      lost: *err (pinned host memory, read by the host without a sync) is set, every output of the
 //      call is written as NaN (a missed check cannot pass stale slots off as a sum) and the rank's
@@ -58,6 +60,7 @@ struct Args {
   uint64_t* ctr;                             // [0] epoch of the last call, [1] arrival ticket (local memory)
   int* err;                                  // != 0: a peer never arrived / diverged (host-mapped)
   int world, rank, n, chunk, mode;
+  uint32_t sig;                              // call_sig(mode, n, 4)
   int64_t spin_limit;
   float* out;                                // SUM: [n] fp32
   uint16_t* res;                             // FOLD_RES / SET_RES: bf16 residual stream [n]
@@ -77,17 +80,28 @@ __device__ __forceinline__ void advance_epoch(uint64_t* ctr, uint64_t e) {
   }
 }
 
-// Poll a peer's flag for epoch e.  Legal values are e - 2 (the peer has not reached this call yet)
-// and e (published); anything past e means the peer skipped a call (or this rank did).  Returns false
-// for a lost peer: bounded spin expired or a diverged epoch.
-__device__ __forceinline__ bool wait_peer(const uint64_t* pf, uint64_t e, int64_t spin_limit) {
+// A flag word is (epoch << 8) | signature of the call (its kind and size): ranks whose call sequences
+// drifted apart by whole calls publish the expected epoch for a DIFFERENT call, which the signature
+// exposes (epochs alone re-align after one skipped call).
+__host__ __device__ __forceinline__ uint32_t call_sig(int mode, int64_t n, int es) {
+  uint64_t h = (uint64_t)n * 0x9E3779B97F4A7C15ull ^ ((uint64_t)(mode + 1) << 40) ^ ((uint64_t)es << 48);
+  h ^= h >> 29;
+  return (uint32_t)(h & 0xFF);
+}
+__device__ __forceinline__ uint64_t flag_word(uint64_t e, uint32_t sig) { return (e << 8) | sig; }
+
+// Poll a peer's flag for epoch e.  Legal values are those of e - 2 (the peer has not reached this call
+// yet) and e with this call's signature; a later epoch, or epoch e for another kind / size of call,
+// means the peers' call sequences diverged.  Returns false for a lost peer: bounded spin expired or
+// diverged.
+__device__ __forceinline__ bool wait_peer(const uint64_t* pf, uint64_t e, uint32_t sig, int64_t spin_limit) {
   int64_t it = 0;
   uint64_t v;
-  while ((v = __hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) < e) {
+  while (((v = __hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> 8) < e) {
     __builtin_amdgcn_s_sleep(2);
     if (++it > spin_limit) return false;
   }
-  return v == e;
+  return v == flag_word(e, sig);
 }
 
 // A rank that lost a peer poisons ALL its flags (both parities, every block): a peer still running
@@ -125,7 +139,7 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: peers may sit on other GPUs
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(a.flag + par * kMaxBlocks + b, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.flag + par * kMaxBlocks + b, flag_word(e, a.sig), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // (rank loops unrolled with static indices: a runtime index into the kernel-argument arrays would
   // copy them to scratch)
@@ -135,7 +149,7 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
     if (r == tid) pf = a.peer_flag[r] + par * kMaxBlocks + b;
   if (tid == 0) lost_s = 0;
   __syncthreads();
-  if (tid < a.world && tid != a.rank && !wait_peer(pf, e, a.spin_limit)) {
+  if (tid < a.world && tid != a.rank && !wait_peer(pf, e, a.sig, a.spin_limit)) {
     lost_s = 1;
     __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -219,6 +233,7 @@ struct CollArgs {
   uint64_t* ctr;
   int* err;
   int world, rank, es, mode;   // es: element bytes (2 | 4); mode 0 AG, 1 RS
+  uint32_t sig;                // call_sig(4 + mode, n, es)
   int64_t n, chunk, spin_limit;
   char* out;
 };
@@ -250,7 +265,7 @@ __global__ void __launch_bounds__(kThreads) peer_coll_kernel(CollArgs a) {
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(a.flag + par * kMaxBlocks + b, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.flag + par * kMaxBlocks + b, flag_word(e, a.sig), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const uint64_t* pf = nullptr;
 #pragma unroll
@@ -258,7 +273,7 @@ __global__ void __launch_bounds__(kThreads) peer_coll_kernel(CollArgs a) {
     if (r == tid) pf = a.peer_flag[r] + par * kMaxBlocks + b;
   if (tid == 0) lost_s = 0;
   __syncthreads();
-  if (tid < a.world && tid != a.rank && !wait_peer(pf, e, a.spin_limit)) {
+  if (tid < a.world && tid != a.rank && !wait_peer(pf, e, a.sig, a.spin_limit)) {
     lost_s = 1;
     __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -428,6 +443,7 @@ int peer_ar_run(void* hv, float* in, int zero_in, int mode, int n, float* out, v
   a.rank = h->rank;
   a.n = n;
   a.mode = mode;
+  a.sig = par::call_sig(mode, n, 4);
   // ~1 KiB of fp32 per block keeps every CU's share latency-sized; at most kMaxBlocks blocks
   int blocks = (n + 1023) / 1024;
   blocks = blocks < 1 ? 1 : (blocks > par::kMaxBlocks ? par::kMaxBlocks : blocks);
@@ -468,6 +484,7 @@ int peer_coll_run(void* hv, const void* in, void* out, int64_t n, int es, int mo
   a.es = es;
   a.mode = mode;
   a.n = n;
+  a.sig = par::call_sig(4 + mode, n, es);
   // 64 KiB of this rank's elements per block (latency-bound below that), at most kMaxBlocks blocks
   int64_t blocks = (n * es + 65535) / 65536;
   blocks = blocks < 1 ? 1 : (blocks > par::kMaxBlocks ? par::kMaxBlocks : blocks);

@@ -16,14 +16,9 @@ The gloo backend (CPU test harness) lacks the "_base" flat-tensor collectives; t
 emulated there with list all-gathers / all-reduce + slice, so the parallel code paths are the same
 on CPU and GPU.
 
-Native RCCL layer (`NXD_NATIVE_COMM=1` or `set_native_comm(True)`): GPU tensors on an RCCL group go
-through parallel/native_comm.NativeCommunicator (csrc/comm.cpp) instead of the ProcessGroup: the
-DP bucket reduce-scatter / all-gather / all-reduce of parallel/grad_buffer.py and the coalesced
-sequence-parallel norm-gradient all-reduce (`all_reduce_coalesced`: one RCCL group launch for the
-list, no concatenation copy) run on the communicator's high-priority HIP stream, ordered by
-events.  One communicator per process group, created at the group's first collective (all its
-ranks get there together).  Off by default: torch's ProcessGroupNCCL is the path the multi-GPU
-bench has run; CPU / gloo tensors always take the torch path.
+Direct-peer layer (parallel/peer_allreduce.py over csrc/peer_allreduce.hip): the tensor-parallel
+decode all-reduces run on it by default, the sequence-parallel all-gather / reduce-scatter with
+`NXD_SP_PEER=1`.  Everything else is torch's ProcessGroupNCCL (RCCL over xGMI).
 """
 
 from __future__ import annotations
@@ -117,32 +112,6 @@ class _Done:
         return True
 
 
-_native = os.environ.get("NXD_NATIVE_COMM", "0") == "1"
-_native_comms: Dict[object, object] = {}
-
-
-def set_native_comm(enabled: bool) -> None:
-    global _native
-    _native = bool(enabled)
-
-
-def native_comm_enabled() -> bool:
-    return _native
-
-
-def _native_for(group, t: torch.Tensor):
-    """The native communicator for `group` when the native layer applies to tensor `t`."""
-    if not _native or not t.is_cuda or _is_gloo(group):
-        return None
-    key = group if group is not None else "world"
-    c = _native_comms.get(key)
-    if c is None:
-        from .native_comm import NativeCommunicator
-
-        c = _native_comms[key] = NativeCommunicator(group)
-    return c
-
-
 # NXD_SP_PEER=1: all-gather / reduce-scatter of GPU tensors (the sequence-parallel activations) over
 # IPC-mapped peer buffers, one kernel per call reading every peer directly
 # (parallel/peer_allreduce.py PeerCollectives; any group backend, so ranks sharing one GPU over gloo
@@ -177,12 +146,6 @@ def check_peer_collectives(sync: bool = True) -> None:
         c.check()
 
 
-def _native_result(work, async_op: bool, op: str, t: torch.Tensor):
-    if not async_op:
-        return None
-    return _track(work if work is not None else _Done(), op, t)
-
-
 def _is_gloo(group) -> bool:
     try:
         return dist.get_backend(group) == "gloo"
@@ -197,9 +160,6 @@ def all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, asy
     if pc is not None and (inp.numel() % 8 == 0):
         w = pc.all_gather(out, inp, async_op=async_op)
         return _track(w, "all_gather", out) if async_op else None
-    nc = _native_for(group, out)
-    if nc is not None:
-        return _native_result(nc.all_gather([out], [inp.contiguous()], async_op=async_op), async_op, "all_gather", out)
     if not _is_gloo(group):
         w = dist.all_gather_into_tensor(out, inp.contiguous(), group=group, async_op=async_op)
         return _track(w, "all_gather", out) if async_op else w
@@ -221,10 +181,6 @@ def reduce_scatter_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, asyn
     if pc is not None and out.numel() % 8 == 0 and inp.dtype in (torch.bfloat16, torch.float32):
         w = pc.reduce_scatter(out, inp, async_op=async_op)
         return _track(w, "reduce_scatter", inp) if async_op else None
-    nc = _native_for(group, inp) if op == dist.ReduceOp.SUM else None
-    if nc is not None:
-        w = nc.reduce_scatter([out], [inp.contiguous()], "sum", async_op=async_op)
-        return _native_result(w, async_op, "reduce_scatter", inp)
     if not _is_gloo(group):
         w = dist.reduce_scatter_tensor(out, inp.contiguous(), op=op, group=group, async_op=async_op)
         return _track(w, "reduce_scatter", inp) if async_op else w
@@ -238,24 +194,16 @@ def reduce_scatter_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, asyn
 
 def all_reduce(t: torch.Tensor, group=None, async_op: bool = False, op=dist.ReduceOp.SUM):
     _fr("all_reduce", t, group)
-    nc = _native_for(group, t) if op == dist.ReduceOp.SUM and t.is_contiguous() else None
-    if nc is not None:
-        return _native_result(nc.all_reduce([t], "sum", async_op=async_op), async_op, "all_reduce", t)
     w = dist.all_reduce(t, op=op, group=group, async_op=async_op)
     return _track(w, "all_reduce", t) if async_op else w
 
 
 def all_reduce_coalesced(tensors: List[torch.Tensor], group=None) -> None:
-    """In-place sum of every tensor over `group`: one RCCL group launch on the native layer, else
-    one all-reduce of their concatenation (copied back)."""
+    """In-place sum of every tensor over `group`: one all-reduce of their concatenation (copied back)."""
     tensors = [t for t in tensors if t.numel()]
     if not tensors or dist.get_world_size(group=group) == 1:
         return
     _fr(f"all_reduce_coalesced[{len(tensors)}]", tensors[0], group)
-    nc = _native_for(group, tensors[0]) if all(t.is_contiguous() for t in tensors) else None
-    if nc is not None:
-        nc.all_reduce(list(tensors), "sum", async_op=False)
-        return
     if len(tensors) == 1:
         dist.all_reduce(tensors[0], group=group)
         return

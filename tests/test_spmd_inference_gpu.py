@@ -137,11 +137,14 @@ def _teacher_forced(server, ids, P, steps, fused):
     return torch.stack(outs, 1)
 
 
-def test_tp2_fused_decode_matches_unfused_like_tp1():
+@pytest.mark.parametrize("deterministic,batch", [(True, 2), (False, 2), (False, 4), (False, 8)])
+def test_tp2_fused_decode_matches_unfused_like_tp1(deterministic, batch):
     """TP = 2 decode on the fused kernels with the one-shot peer all-reduce (two ranks on the GPU):
     against the same server's unfused decode (same prefill KV cache, so only the decode path differs)
     it differs no more than the TP = 1 fused decode does from the TP = 1 unfused one -- the two fused
-    paths round identically; the TP=2 partials are summed in fp32."""
+    paths round identically; the TP=2 partials are summed in fp32.  deterministic=False (the serving
+    default) takes the fp32-atomic attention + o_proj launch at batch <= 2 (its accumulator summed by
+    the peer kernel with zero_in) and the MFMA row GEMVs with fp32 partials from batch 4."""
     from neuronx_distributed_llama3_2_amd.inference.spmd_server import SpmdGenerationServer
 
     cfg = _cfg("llama3.2-1b")
@@ -150,8 +153,8 @@ def test_tp2_fused_decode_matches_unfused_like_tp1():
     torch.save(_random_full_state(cfg, "llama3.2-1b", seed=3), path)
     torch.manual_seed(9)
     P, steps = 24, 12
-    ids = torch.randint(3, cfg.vocab_size, (2, P + steps))
-    kw = dict(batch_size=2, seq_len=128, max_context_length=96, deterministic=True, use_hip_graphs=False)
+    ids = torch.randint(3, cfg.vocab_size, (batch, P + steps))
+    kw = dict(batch_size=batch, seq_len=128, max_context_length=96, deterministic=deterministic, use_hip_graphs=False)
     rel = {}
     for tp in (1, 2):
         server = SpmdGenerationServer.from_full_state_dict(cfg.to_dict(), path, tp, kw, dtype="bfloat16")
@@ -191,3 +194,29 @@ def test_tp2_decode_hipgraph_on_peer_kernels():
         finally:
             server.close()
     assert torch.equal(outs[True], outs[False])
+
+
+def test_tp2_decode_lost_peer_raises():
+    """A TP = 2 rank that silently skips one decode all-reduce (NXD_PEER_AR_DROP, test hook): its peer's
+    call sees the expected epoch with another call's signature (or times out), writes NaN and poisons
+    its flags; generate() raises on the ranks instead of returning tokens."""
+    from neuronx_distributed_llama3_2_amd.inference.spmd_server import SpmdGenerationServer
+
+    cfg = _cfg("tiny")
+    d = tempfile.mkdtemp()
+    path = os.path.join(d, "full.pt")
+    torch.save(_random_full_state(cfg, "tiny", seed=6), path)
+    ids = torch.randint(3, cfg.vocab_size, (2, 16), generator=torch.Generator().manual_seed(2))
+    kw = dict(batch_size=2, seq_len=128, max_context_length=96, deterministic=True, use_hip_graphs=False,
+              decode_graph_steps=4)
+    os.environ.update(NXD_PEER_AR_DROP="1:10", NXD_PEER_AR_SPIN_LIMIT="200000")
+    try:
+        server = SpmdGenerationServer.from_full_state_dict(cfg.to_dict(), path, 2, kw, dtype="bfloat16")
+    finally:
+        os.environ.pop("NXD_PEER_AR_DROP")
+        os.environ.pop("NXD_PEER_AR_SPIN_LIMIT")
+    try:
+        with pytest.raises(RuntimeError, match="peer all-reduce"):
+            server.generate(ids, max_new_tokens=24, eos_token_id=-1)
+    finally:
+        server.close()
