@@ -25,6 +25,7 @@ int peer_ar_open(void*, int, int, const void*);
 int peer_ar_run(void*, float*, int, int, int, float*, void*, const float*, int, hipStream_t);
 int peer_ar_error(void*);
 void peer_ar_set_error(void*, int);
+void peer_ar_set_spin_limit(void*, int64_t);
 void peer_ar_destroy(void*);
 }
 
@@ -124,6 +125,7 @@ void register_comm(pybind11::module& m) {
   m.def("peer_ar_gather", &peer_ar_gather);
   m.def("peer_coll", &peer_coll);
   m.def("peer_ar_error", [](int64_t h) { return nxd::peer_ar_error(reinterpret_cast<void*>(h)); });
+  m.def("peer_ar_set_spin_limit", [](int64_t h, int64_t v) { nxd::peer_ar_set_spin_limit(reinterpret_cast<void*>(h), v); });
   m.def("peer_ar_set_error", [](int64_t h, int v) { nxd::peer_ar_set_error(reinterpret_cast<void*>(h), v); });
   m.def("peer_ar_destroy", [](int64_t h) { nxd::peer_ar_destroy(reinterpret_cast<void*>(h)); });
 }

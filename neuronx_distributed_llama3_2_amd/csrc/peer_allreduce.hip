@@ -208,7 +208,17 @@ struct Handle {
   uint64_t* ctr = nullptr;
   int* err = nullptr;          // device-side pointer the kernels store to
   int* err_host = nullptr;     // the same word, host-mapped pinned memory (nullptr: device memory)
+  int64_t spin_limit = -1;     // polls before a peer counts as lost (< 0: NXD_PEER_AR_SPIN_LIMIT)
 };
+
+int64_t env_spin_limit() {
+  static const int64_t limit = [] {
+    const char* e = getenv("NXD_PEER_AR_SPIN_LIMIT");
+    return e ? atoll(e) : (int64_t)1 << 24;   // ~ seconds of s_sleep polling, then give up
+  }();
+  return limit;
+}
+int64_t spin_limit_of(const Handle* h) { return h->spin_limit >= 0 ? h->spin_limit : env_spin_limit(); }
 
 constexpr size_t kFlagBytes = 2 * kMaxBlocks * sizeof(uint64_t);
 constexpr size_t kHeader = 4096;
@@ -449,11 +459,7 @@ int peer_ar_run(void* hv, float* in, int zero_in, int mode, int n, float* out, v
   blocks = blocks < 1 ? 1 : (blocks > par::kMaxBlocks ? par::kMaxBlocks : blocks);
   a.chunk = ((n + blocks - 1) / blocks + 3) / 4 * 4;
   blocks = (n + a.chunk - 1) / a.chunk;
-  static const int64_t limit = [] {
-    const char* e = getenv("NXD_PEER_AR_SPIN_LIMIT");
-    return e ? atoll(e) : (int64_t)1 << 24;   // ~ seconds of s_sleep polling, then give up
-  }();
-  a.spin_limit = limit;
+  a.spin_limit = par::spin_limit_of(h);
   a.out = out;
   a.res = static_cast<uint16_t*>(res);
   a.xadd = xadd;
@@ -490,11 +496,7 @@ int peer_coll_run(void* hv, const void* in, void* out, int64_t n, int es, int mo
   blocks = blocks < 1 ? 1 : (blocks > par::kMaxBlocks ? par::kMaxBlocks : blocks);
   a.chunk = ((n + blocks - 1) / blocks + 7) / 8 * 8;
   blocks = (n + a.chunk - 1) / a.chunk;
-  static const int64_t limit = [] {
-    const char* e = getenv("NXD_PEER_AR_SPIN_LIMIT");
-    return e ? atoll(e) : (int64_t)1 << 24;
-  }();
-  a.spin_limit = limit;
+  a.spin_limit = par::spin_limit_of(h);
   a.out = static_cast<char*>(out);
   hipLaunchKernelGGL(par::peer_coll_kernel, dim3((unsigned)blocks), dim3(par::kThreads), 0, stream, a);
   return (int)hipGetLastError();
@@ -509,6 +511,10 @@ int peer_ar_error(void* hv) {
   if (hipMemcpy(&v, h->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return v;
 }
+
+// Per-handle bound of the peer wait (< 0: back to NXD_PEER_AR_SPIN_LIMIT).  The init self-test runs
+// with a generous one: the ranks' first launches (code-object load) can be milliseconds apart.
+void peer_ar_set_spin_limit(void* hv, int64_t v) { static_cast<par::Handle*>(hv)->spin_limit = v; }
 
 // Host-side test hook: a lost peer injected without a GPU fault (tests only).
 void peer_ar_set_error(void* hv, int v) {

@@ -404,6 +404,12 @@ class LlamaForCausalLMInference:
                                                 use_graph=self._decode_graphs_allowed())
         return g
 
+    def _peer_decode(self) -> bool:
+        """True once this model's TP decode all-reduces run on the one-shot peer kernels (built at the
+        first decode step)."""
+        st = getattr(self.model, "_tp_dec", None)
+        return st is not None and type(st["ar"]).__name__ == "PeerAllReduce"
+
     @torch.no_grad()
     def generate(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                  max_new_tokens: Optional[int] = None, do_sample: bool = False, top_k: int = 1,
@@ -463,14 +469,12 @@ class LlamaForCausalLMInference:
             uni = torch.rand((st.max_steps, Bp), device=dev, generator=gen)
             st.load(first, lengths, torch.arange(Bp, device=dev), uni)
             g = self._graph(Bp, sampler)
-            st_tp = getattr(self.model, "_tp_dec", None)
-            peer = st_tp is not None and type(st_tp["ar"]).__name__ == "PeerAllReduce"
             todo = max_new_tokens - 1
             done_steps = 0
             while done_steps < todo:
                 g.replay()
                 done_steps += g.steps
-                if peer:
+                if self._peer_decode():
                     # a lost TP peer wrote NaN logits / residuals: fail this generate(), never emit them
                     torch.cuda.current_stream().synchronize()
                     self.model.check_collectives()

@@ -86,8 +86,10 @@ class PeerAllReduce:
         pat = lambda r: (r + 1) * 1000.0 + (i % 61)   # noqa: E731
         inp = pat(self.rank)
         out = torch.empty(n, device="cuda")
+        self.C.peer_ar_set_spin_limit(self.h, 1 << 26)   # first launches may be far apart
         self.C.peer_ar_run(self.h, inp, False, SUM, out, None, None)
         torch.cuda.current_stream().synchronize()
+        self.C.peer_ar_set_spin_limit(self.h, -1)
         want = sum(pat(r) for r in range(self.world))
         return bool(torch.equal(out, want)) and int(self.C.peer_ar_error(self.h)) == 0
 
