@@ -47,6 +47,7 @@ struct Params {
   float* pm;   // natural-log row max
   float* pl;
   int B, T, Hq, Hkv, nsplit;
+  int kps;            // keys per split (multiple of KB; FUSE: unused)
   float scale_log2;   // softmax scale * log2(e)
   // weight prefetch riding on the (tiny) attention grid: workgroups >= attn_wgs stream the two
   // byte ranges through the memory hierarchy so the next projections (o_proj, gate_up) find them
@@ -156,7 +157,8 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
 #pragma unroll
   for (int i = 0; i < NDT; ++i) o[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int kend = min(slen, (split + 1) * KPS);
+  // FUSE: the whole cache in one pass per workgroup (no key splits, no merge launch)
+  const int kend = FUSE ? slen : min(slen, (split + 1) * p.kps);
   // K fragments and the V chunk of the NEXT chunk are loaded while this one runs its softmax and P.V
   u32x4_t kf[4][NS], vv[VL];
   auto load_chunk = [&](int k0) {
@@ -172,7 +174,7 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
       for (int s = 0; s < NS; ++s) kf[kt][s] = *reinterpret_cast<const u32x4_t*>(kr + 32 * s);
     }
   };
-  int k0 = split * KPS + wid * KB;
+  int k0 = split * p.kps + wid * KB;
   if (k0 < kend) load_chunk(k0);
   // FUSE: the Wo block is issued AFTER the q and first K / V loads.  vmcnt retires in issue order:
   // issued first (round 3), the cold-HBM Wo loads had to land before the first score MFMA could
@@ -368,7 +370,20 @@ int decode_attn2_launch(const void* q, const int64_t* qs, const void* kc, const 
   p.out = (uint16_t*)out; p.o_sb = os[0]; p.o_st = os[1]; p.o_sh = os[2];
   p.po = po; p.pm = pm; p.pl = pl;
   p.B = B; p.T = T; p.Hq = Hq; p.Hkv = Hkv;
-  p.nsplit = Lmax <= dattn::KPS ? 1 : (Lmax + dattn::KPS - 1) / dattn::KPS;
+  // Keys per split: enough splits that the (batch, kv head, split) grid reaches ~NXD_DECODE_ATTN_WGS
+  // workgroups (default 256) -- the KV cache streams from HBM at the per-CU rate, so 24 workgroups on a
+  // 2,304-key cache took 9.8 us -- between 128 keys (the caller's partial buffers hold Lmax / 128
+  // splits) and 1,024 (one pass of the 8 waves x 2 chunks).
+  static const int target = [] {
+    const char* e = getenv("NXD_DECODE_ATTN_WGS");
+    const int v = e ? atoi(e) : 256;
+    return v > 0 ? v : 256;
+  }();
+  int kps = (int)(((int64_t)Lmax * B * Hkv + target - 1) / target);
+  kps = (kps + dattn::KB - 1) / dattn::KB * dattn::KB;
+  kps = kps < 128 ? 128 : (kps > dattn::KPS ? dattn::KPS : kps);
+  p.kps = kps;
+  p.nsplit = (Lmax + kps - 1) / kps;
   p.scale_log2 = scale * 1.4426950408889634f;
   *nsplit_out = p.nsplit;
   // D = 64: 8 waves (<= 2 chunks each per 1024-key split); D = 128: 4 waves (LDS: V tiles + merge)
@@ -399,13 +414,20 @@ int decode_attn2_launch(const void* q, const int64_t* qs, const void* kc, const 
 
 // Fused decode attention + o_proj (see FUSE above): oacc [B*T, Hout] fp32 must be zero on entry
 // (the down projection's RESID epilogue re-zeroes it).  Returns -1 when the shape is not covered:
-// one key split (Lmax <= 1024), M = G*T <= 16, D in {64, 128}, Wo blocks of <= 4 register passes.
+// cache capacity Lmax <= NXD_DECODE_ATTN_OPROJ_MAXL (default 4096: every workgroup of a kv head walks
+// the whole cache once -- at the notebook's 2,304-key cache that replaced a 24-workgroup split
+// attention + merge launch + o_proj launch), M = G*T <= 16, D in {64, 128}, Wo blocks of <= 4
+// register passes.
 int decode_attn_oproj_launch(const void* q, const int64_t* qs, const void* kc, const void* vc, const int64_t* cs,
                              const int* cache_idx, const int* seq_len, const void* wo, int64_t ldwo, int Hout, float* oacc,
                              int B, int T, int Hq, int Hkv, int D, int Lmax, float scale, hipStream_t stream) {
   if (Hkv <= 0 || Hq % Hkv) return -1;
   const int G = Hq / Hkv, M = G * T;
-  if (M > 16 || (D != 64 && D != 128) || Lmax > dattn::KPS || (G * D) % 32 || ldwo % 8) return -1;
+  static const int maxl = [] {
+    const char* e = getenv("NXD_DECODE_ATTN_OPROJ_MAXL");
+    return e ? atoi(e) : 4096;
+  }();
+  if (M > 16 || (D != 64 && D != 128) || Lmax > maxl || (G * D) % 32 || ldwo % 8) return -1;
   const int nwv = D == 64 ? 8 : 4;
   const int nt = 64 * nwv, tpr = (G * D) / 32;
   if (tpr > 64 || 64 % tpr || nt % tpr) return -1;

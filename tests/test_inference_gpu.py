@@ -15,11 +15,11 @@ def _cfg():
                        rope_theta=500000.0, tie_word_embeddings=True, eos_token_id=2)
 
 
-def _model(cfg, sd, dtype, graphs=True, steps=8, device=None):
+def _model(cfg, sd, dtype, graphs=True, steps=8, device=None, seq_len=256, ctx=128):
     from neuronx_distributed_llama3_2_amd.inference import InferenceConfig, LlamaForCausalLMInference
     from neuronx_distributed_llama3_2_amd.models.llama.convert import hf_to_nxd
 
-    icfg = InferenceConfig(batch_size=2, seq_len=256, max_context_length=128, use_hip_graphs=graphs,
+    icfg = InferenceConfig(batch_size=2, seq_len=seq_len, max_context_length=ctx, use_hip_graphs=graphs,
                            decode_graph_steps=steps)
     m = LlamaForCausalLMInference(cfg, icfg, dtype=dtype, device=device, init_weights=False)
     m._load_full(hf_to_nxd(sd, cfg))
@@ -256,6 +256,40 @@ def test_fused_attention_oproj_matches_two_launches(monkeypatch, hidden, heads, 
     lf = f.forward_tokens(last, pos, sid, clen).float()
     monkeypatch.setattr(model_base, "_ATTN_OPROJ", False)
     lu = u.forward_tokens(last, pos, sid, clen).float()
+    assert ((lf - lu).abs().max() / lu.abs().max()).item() < 2e-2
+
+
+@pytest.mark.parametrize("hidden,heads,kv", [(2048, 32, 8), (1024, 8, 2)])   # D = 64, 128
+def test_fused_attention_oproj_long_context(monkeypatch, hidden, heads, kv):
+    """The fused attention + o_proj launch on a cache past one 1,024-key split (the notebook config's
+    2,048-token context + 256 new): each workgroup walks the whole cache; one decode step against the
+    split attention + merge + o_proj launches on identical caches."""
+    from transformers import LlamaConfig, LlamaForCausalLM as HF
+    from neuronx_distributed_llama3_2_amd.inference import model_base
+
+    cfg = LlamaConfig(hidden_size=hidden, intermediate_size=2 * hidden, num_hidden_layers=2, num_attention_heads=heads,
+                      num_key_value_heads=kv, vocab_size=1000, max_position_embeddings=4096, rms_norm_eps=1e-5,
+                      rope_theta=500000.0, tie_word_embeddings=True, eos_token_id=2)
+    torch.manual_seed(0)
+    sd = {k: v.detach().clone() for k, v in HF(cfg).state_dict().items()}
+    torch.manual_seed(7)
+    P = 1800
+    ids = torch.randint(3, cfg.vocab_size, (2, P))
+    m = _model(cfg, sd, torch.bfloat16, graphs=False, steps=1, device=torch.device("cuda"), seq_len=2304, ctx=2048)
+    m.generate(ids, max_new_tokens=2, eos_token_id=-1)    # fills the cache with P + 1 positions
+    f = m.model
+    last = torch.randint(3, cfg.vocab_size, (2, 1), device="cuda")
+    pos = torch.full((2, 1), P + 1, dtype=torch.int64, device="cuda")
+    sid = torch.arange(2, device="cuda")
+    clen = torch.full((2,), P + 2, dtype=torch.int32, device="cuda")
+    saved = f.kv_cache.clone()
+    monkeypatch.setattr(model_base, "_ATTN_OPROJ", True)
+    lf = f.forward_tokens(last, pos, sid, clen).float()
+    buf = getattr(f, "_oacc_buf", None)
+    assert buf is not None and int((buf != 0).sum()) == 0, "fused path not taken or accumulator not consumed"
+    f.kv_cache.copy_(saved)
+    monkeypatch.setattr(model_base, "_ATTN_OPROJ", False)
+    lu = f.forward_tokens(last, pos, sid, clen).float()
     assert ((lf - lu).abs().max() / lu.abs().max()).item() < 2e-2
 
 
