@@ -71,7 +71,7 @@ int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, i
 int wgrad_gemm_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int, int, int, int, hipStream_t);
 int wgrad_gemm_choose_splits(int, int, int);
 int decode_attn_oproj_launch(const void*, const int64_t*, const void*, const void*, const int64_t*, const int*, const int*,
-                             const void*, int64_t, int, float*, int, int, int, int, int, int, float, hipStream_t);
+                             const void*, int64_t, int, float*, float*, float*, float*, int, int, int, int, int, int, float, hipStream_t);
 int grouped_rowgemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, hipStream_t);
 int wgrad_gemm_grouped_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int64_t, const int*, int, int,
                               int, int, hipStream_t);
@@ -79,6 +79,8 @@ void wgrad_gemm_set_ablate(int);
 int dense_gemm_launch(int, int, const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, hipStream_t);
 int dense_gemm_choose_splits(int, int, int);
 void dense_gemm_set_pipe(int);
+void decode_attn_set_oproj_maxl(int);
+int decode_attn_oproj_maxl();
 void grouped_rowgemm_set_pp(int);
 void wgrad_gemm_set_pp(int);
 int cu_stream_launch(const void*, void*, int64_t, int, int64_t, hipStream_t);
@@ -513,9 +515,18 @@ bool decode_attn_oproj(at::Tensor q, at::Tensor kc, at::Tensor vc, c10::optional
   }
   if (Hkv <= 0 || Hq % Hkv || Hout > INT32_MAX) return false;
   const int64_t cs[3] = {kc.stride(0), kc.stride(1), kc.stride(2)};
+  // past the fused kernel's one-pass limit: split attention partials (keys per split >= 128), merged
+  // inside the o_proj launch
+  at::Tensor part;
+  float *po = nullptr, *pm = nullptr, *pl = nullptr;
+  if (Lmax > nxd::decode_attn_oproj_maxl()) {
+    const int64_t rows = (int64_t)B * Hkv * ((Lmax + 127) / 128) * ((int64_t)(Hq / Hkv) * T);
+    part = at::empty({rows * (D + 2)}, q.options().dtype(at::kFloat));
+    po = part.data_ptr<float>(); pm = po + rows * D; pl = pm + rows;
+  }
   const int rc = nxd::decode_attn_oproj_launch(q.data_ptr(), qs, kc.data_ptr(), vc.data_ptr(), cs, ci, seq_len.data_ptr<int>(),
-                                               wo.data_ptr(), wo.stride(0), (int)Hout, oacc.data_ptr<float>(), B, T, Hq, Hkv, D,
-                                               Lmax, (float)scale, cur_stream());
+                                               wo.data_ptr(), wo.stride(0), (int)Hout, oacc.data_ptr<float>(), po, pm, pl, B, T,
+                                               Hq, Hkv, D, Lmax, (float)scale, cur_stream());
   if (rc == -1) return false;
   check_rc(rc, "decode_attn_oproj");
   return true;
@@ -1141,6 +1152,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("decode_attn", &decode_attn);
   m.def("decode_attn_oproj", &decode_attn_oproj);
+  m.def("decode_attn_set_oproj_maxl", [](int64_t v) { nxd::decode_attn_set_oproj_maxl((int)v); });
   m.def("decode_attn_prefetch", &decode_attn_prefetch);
   m.def("kv_cache_write", &kv_cache_write);
   m.def("argmax_rows", &argmax_rows);

@@ -93,6 +93,46 @@ __device__ __forceinline__ void prefetch_body(const Params& p, int wg, int nwg) 
 typedef __attribute__((address_space(3))) short4_t lds_s4_t;
 typedef short short8_t __attribute__((ext_vector_type(8)));
 
+// FUSE o_proj pieces: thread (row row0 + pass * rpp, 32-column segment) holds its Wo block in
+// registers (<= 4 passes), then adds its rows' dot products with the attention output into oacc.
+__device__ __forceinline__ void load_wo_regs(const Params& p, int row0, int col0, int rpp, u32x4_t (&wreg)[4][4]) {
+  const uint16_t* wb = p.wo + (int64_t)row0 * p.ldwo + col0;
+#pragma unroll
+  for (int np = 0; np < 4; ++np) {
+    if (np < p.NP) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wreg[np][j] = *reinterpret_cast<const u32x4_t*>(wb + (int64_t)np * rpp * p.ldwo + 8 * j);
+    }
+  }
+}
+
+// out[t][row] += sum_c Wo[row][hkv*G*D + c] o[t][c] over this thread's 32 columns, reduced over the
+// tpr threads of a row; of = [M][D] attention output (m = t * G + g)
+template <int D>
+__device__ __forceinline__ void oproj_tail(const Params& p, const float* of, const u32x4_t (&wreg)[4][4], int b, int row0,
+                                           int rpp, int tpr, int seg, int G) {
+  const int c0 = 32 * seg, gg = c0 / D, d0 = c0 % D;
+#pragma unroll
+  for (int np = 0; np < 4; ++np) {
+    if (np >= p.NP) break;
+    float w[32];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) unpack8(wreg[np][j], w + 8 * j);
+    const int row = row0 + np * rpp;
+    for (int tt = 0; tt < p.T; ++tt) {
+      const float* orow = of + (tt * G + gg) * D + d0;
+      float dot = 0.f;
+#pragma unroll
+      for (int j = 0; j < 32; j += 4) {
+        const f32x4_t o4 = *reinterpret_cast<const f32x4_t*>(orow + j);
+        dot += w[j] * o4[0] + w[j + 1] * o4[1] + w[j + 2] * o4[2] + w[j + 3] * o4[3];
+      }
+      for (int off = tpr / 2; off > 0; off >>= 1) dot += __shfl_xor(dot, off, 64);
+      if (seg == 0) unsafeAtomicAdd(p.oacc + (int64_t)(b * p.T + tt) * p.Hout + row, dot);
+    }
+  }
+}
+
 template <int D, int NWV, bool FUSE, bool WO_LATE = true>
 __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
   constexpr int NS = D / 32;      // k-steps of the score MFMA
@@ -123,16 +163,7 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
   const int nr = FUSE ? p.Hout / p.R : 0;
   const int row0 = FUSE ? ((int)blockIdx.x % p.R) * nr + r0 : 0;
   u32x4_t wreg[4][4];
-  auto load_wo = [&]() {
-    const uint16_t* wb = p.wo + (int64_t)row0 * p.ldwo + (int64_t)hkv * G * D + 32 * seg;
-#pragma unroll
-    for (int np = 0; np < 4; ++np) {
-      if (np < p.NP) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) wreg[np][j] = *reinterpret_cast<const u32x4_t*>(wb + (int64_t)np * rpp * p.ldwo + 8 * j);
-      }
-    }
-  };
+  auto load_wo = [&]() { load_wo_regs(p, row0, hkv * G * D + 32 * seg, rpp, wreg); };
   if constexpr (FUSE && !WO_LATE) load_wo();   // round-3 order (A/B: NXD_DECODE_WO_LATE=0)
   const int cb = p.cache_idx ? p.cache_idx[b] : b;
   const int slen = p.seq_len[b];
@@ -308,31 +339,67 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
     }
   }
   if constexpr (FUSE) {
-    // ---- o_proj partial of this head group: out[t][row] += sum_c Wo[row][hkv*G*D + c] o[t][c]
     __syncthreads();
-    const float* of = reinterpret_cast<const float*>(smem);   // [M][D] attention output (m = t * G + g)
-    const int c0 = 32 * seg, gg = c0 / D, d0 = c0 % D;
-#pragma unroll
-    for (int np = 0; np < 4; ++np) {
-      if (np >= p.NP) break;
-      float w[32];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) unpack8(wreg[np][j], w + 8 * j);
-      const int row = row0 + np * rpp;
-      for (int tt = 0; tt < p.T; ++tt) {
-        const float* orow = of + (tt * G + gg) * D + d0;
-        float dot = 0.f;
-#pragma unroll
-        for (int j = 0; j < 32; j += 4) {
-          const f32x4_t o4 = *reinterpret_cast<const f32x4_t*>(orow + j);
-          dot += w[j] * o4[0] + w[j + 1] * o4[1] + w[j + 2] * o4[2] + w[j + 3] * o4[3];
-        }
-        for (int off = tpr / 2; off > 0; off >>= 1) dot += __shfl_xor(dot, off, 64);
-        if (seg == 0) unsafeAtomicAdd(p.oacc + (int64_t)(b * p.T + tt) * p.Hout + row, dot);
-      }
-    }
+    oproj_tail<D>(p, reinterpret_cast<const float*>(smem), wreg, b, row0, rpp, tpr, seg, G);
   }
   if (p.trace != nullptr && tid == 0) p.trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
+// Keys per split: enough splits that the (batch, kv head, split) grid reaches ~NXD_DECODE_ATTN_WGS
+// workgroups (default 128) -- the KV cache streams from HBM at the per-CU rate, so 24 workgroups on a
+// 2,304-key cache took 9.8 us -- between 128 keys (the caller's partial buffers hold Lmax / 128
+// splits) and 1,024 (one pass of the 8 waves x 2 chunks).  0.786 -> 0.726 ms/token at the notebook
+// config (profiles/r6_decode/attn_split_ab.txt).
+static int keys_per_split(int Lmax, int B, int Hkv) {
+  static const int target = [] {
+    const char* e = getenv("NXD_DECODE_ATTN_WGS");
+    const int v = e ? atoi(e) : 128;
+    return v > 0 ? v : 128;
+  }();
+  int kps = (int)(((int64_t)Lmax * B * Hkv + target - 1) / target);
+  kps = (kps + KB - 1) / KB * KB;
+  return kps < 128 ? 128 : (kps > KPS ? KPS : kps);
+}
+
+// Split attention's partials -> merged attention row block (bf16-rounded, as the merge kernel's
+// output the o_proj GEMV would read) -> this workgroup's o_proj partial, fp32 atomics into oacc: the
+// long-context form of FUSE (one launch instead of the merge + o_proj pair).  Grid (batch, kv head,
+// R row chunks), the split weights of each query row in LDS.
+template <int D, int NWV>
+__global__ void __launch_bounds__(64 * NWV) merge_oproj_kernel(Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* of = reinterpret_cast<float*>(smem);   // [M][D] merged attention output
+  float* wts = of + 16 * D;                     // [nsplit][16] normalised split weights
+  const int tid = threadIdx.x;
+  const int bh = (int)blockIdx.x / p.R, b = bh / p.Hkv, hkv = bh % p.Hkv;
+  const int G = p.Hq / p.Hkv, M = G * p.T;
+  const int tpr = (G * D) / 32, seg = tid % tpr, r0 = tid / tpr, rpp = (64 * NWV) / tpr;
+  const int row0 = ((int)blockIdx.x % p.R) * (p.Hout / p.R) + r0;
+  u32x4_t wreg[4][4];
+  load_wo_regs(p, row0, hkv * G * D + 32 * seg, rpp, wreg);
+  const int64_t pb = (int64_t)bh * p.nsplit * M;
+  if (tid < M) {
+    float gm = -INFINITY;
+    for (int s = 0; s < p.nsplit; ++s) gm = fmaxf(gm, p.pm[pb + (int64_t)s * M + tid]);
+    float L = 0.f;
+    for (int s = 0; s < p.nsplit; ++s) {
+      const float ms = p.pm[pb + (int64_t)s * M + tid];
+      const float w = ms == -INFINITY ? 0.f : __expf(ms - gm);
+      wts[s * 16 + tid] = w;
+      L += w * p.pl[pb + (int64_t)s * M + tid];
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    for (int s = 0; s < p.nsplit; ++s) wts[s * 16 + tid] *= inv;
+  }
+  __syncthreads();
+  for (int it = tid; it < M * D; it += 64 * NWV) {
+    const int m = it / D, d = it % D;
+    float acc = 0.f;
+    for (int s = 0; s < p.nsplit; ++s) acc += wts[s * 16 + m] * p.po[(pb + (int64_t)s * M + m) * D + d];
+    of[it] = bf2f(f2bf(acc));
+  }
+  __syncthreads();
+  oproj_tail<D>(p, of, wreg, b, row0, rpp, tpr, seg, G);
 }
 
 // Pending prefetch of the next decode_attn2 launch (set by decode_attn_set_prefetch, consumed by
@@ -370,18 +437,7 @@ int decode_attn2_launch(const void* q, const int64_t* qs, const void* kc, const 
   p.out = (uint16_t*)out; p.o_sb = os[0]; p.o_st = os[1]; p.o_sh = os[2];
   p.po = po; p.pm = pm; p.pl = pl;
   p.B = B; p.T = T; p.Hq = Hq; p.Hkv = Hkv;
-  // Keys per split: enough splits that the (batch, kv head, split) grid reaches ~NXD_DECODE_ATTN_WGS
-  // workgroups (default 256) -- the KV cache streams from HBM at the per-CU rate, so 24 workgroups on a
-  // 2,304-key cache took 9.8 us -- between 128 keys (the caller's partial buffers hold Lmax / 128
-  // splits) and 1,024 (one pass of the 8 waves x 2 chunks).
-  static const int target = [] {
-    const char* e = getenv("NXD_DECODE_ATTN_WGS");
-    const int v = e ? atoi(e) : 256;
-    return v > 0 ? v : 256;
-  }();
-  int kps = (int)(((int64_t)Lmax * B * Hkv + target - 1) / target);
-  kps = (kps + dattn::KB - 1) / dattn::KB * dattn::KB;
-  kps = kps < 128 ? 128 : (kps > dattn::KPS ? dattn::KPS : kps);
+  const int kps = dattn::keys_per_split(Lmax, B, Hkv);
   p.kps = kps;
   p.nsplit = (Lmax + kps - 1) / kps;
   p.scale_log2 = scale * 1.4426950408889634f;
@@ -412,22 +468,36 @@ int decode_attn2_launch(const void* q, const int64_t* qs, const void* kc, const 
   return (int)hipGetLastError();
 }
 
+namespace dattn {
+int g_oproj_maxl = -1;   // NXD_DECODE_ATTN_OPROJ_MAXL, or decode_attn_set_oproj_maxl
+}
+void decode_attn_set_oproj_maxl(int v) { dattn::g_oproj_maxl = v; }
+int decode_attn_oproj_maxl() {
+  if (dattn::g_oproj_maxl < 0) {
+    const char* e = getenv("NXD_DECODE_ATTN_OPROJ_MAXL");
+    dattn::g_oproj_maxl = e ? atoi(e) : 1024;
+  }
+  return dattn::g_oproj_maxl;
+}
+
 // Fused decode attention + o_proj (see FUSE above): oacc [B*T, Hout] fp32 must be zero on entry
 // (the down projection's RESID epilogue re-zeroes it).  Returns -1 when the shape is not covered:
-// cache capacity Lmax <= NXD_DECODE_ATTN_OPROJ_MAXL (default 4096: every workgroup of a kv head walks
-// the whole cache once -- at the notebook's 2,304-key cache that replaced a 24-workgroup split
-// attention + merge launch + o_proj launch), M = G*T <= 16, D in {64, 128}, Wo blocks of <= 4
-// register passes.
+// cache capacity Lmax <= NXD_DECODE_ATTN_OPROJ_MAXL (default 1024: every workgroup of a kv head walks
+// the whole cache; past that the split attention, whose keys per split fill the GPU, + merge + o_proj
+// launches win -- 0.726 vs 0.774 ms/token at the notebook's 2,304-key cache,
+// profiles/r6_decode/attn_split_ab.txt), M = G*T <= 16, D in {64, 128}, Wo blocks of <= 4 register
+// passes.
 int decode_attn_oproj_launch(const void* q, const int64_t* qs, const void* kc, const void* vc, const int64_t* cs,
                              const int* cache_idx, const int* seq_len, const void* wo, int64_t ldwo, int Hout, float* oacc,
-                             int B, int T, int Hq, int Hkv, int D, int Lmax, float scale, hipStream_t stream) {
+                             float* po, float* pm, float* pl, int B, int T, int Hq, int Hkv, int D, int Lmax, float scale,
+                             hipStream_t stream) {
   if (Hkv <= 0 || Hq % Hkv) return -1;
   const int G = Hq / Hkv, M = G * T;
-  static const int maxl = [] {
-    const char* e = getenv("NXD_DECODE_ATTN_OPROJ_MAXL");
-    return e ? atoi(e) : 4096;
-  }();
-  if (M > 16 || (D != 64 && D != 128) || Lmax > maxl || (G * D) % 32 || ldwo % 8) return -1;
+  const int maxl = decode_attn_oproj_maxl();
+  // past maxl: split attention into the partials, then merge + o_proj (needs the partial buffers:
+  // [B * Hkv * ceil(Lmax / 128) * M] rows of D, plus the two stats)
+  const bool split = Lmax > maxl && po != nullptr && dattn::keys_per_split(Lmax, B, Hkv) < Lmax;
+  if (M > 16 || (D != 64 && D != 128) || (Lmax > maxl && !split) || (G * D) % 32 || ldwo % 8) return -1;
   const int nwv = D == 64 ? 8 : 4;
   const int nt = 64 * nwv, tpr = (G * D) / 32;
   if (tpr > 64 || 64 % tpr || nt % tpr) return -1;
@@ -454,8 +524,28 @@ int decode_attn_oproj_launch(const void* q, const int64_t* qs, const void* kc, c
   p.wo = (const uint16_t*)wo; p.ldwo = ldwo; p.oacc = oacc; p.Hout = Hout; p.R = R; p.NP = Hout / R / rpp;
   p.attn_wgs = B * Hkv * R;
   p.trace = dattn::g_trace;
-  const size_t lds = (size_t)nwv * dattn::KB * D * 2 + (size_t)nwv * 16 * D * 4 + (size_t)2 * nwv * 16 * 4;
   const dim3 grid(p.attn_wgs), block(nt);
+  if (split) {
+    const int kps = dattn::keys_per_split(Lmax, B, Hkv), ns = (Lmax + kps - 1) / kps;
+    const size_t mlds = (size_t)16 * D * 4 + (size_t)ns * 16 * 4;
+    if (mlds > 64 * 1024) return -1;
+    int ns2 = 0;
+    const int64_t no_out[3] = {0, 0, 0};
+    const int rc = decode_attn2_launch(q, qs, kc, vc, cs, cache_idx, seq_len, po, pm, pl, nullptr, no_out, B, T, Hq, Hkv,
+                                       D, Lmax, scale, &ns2, stream);
+    if (rc != 0) return rc;
+    if (ns2 != ns) return 3;   // the attention launch split differently: never write the output through null
+    p.nsplit = ns; p.po = po; p.pm = pm; p.pl = pl;
+    if (D == 64) {
+      (void)hipFuncSetAttribute((const void*)dattn::merge_oproj_kernel<64, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlds);
+      hipLaunchKernelGGL((dattn::merge_oproj_kernel<64, 8>), grid, block, mlds, stream, p);
+    } else {
+      (void)hipFuncSetAttribute((const void*)dattn::merge_oproj_kernel<128, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlds);
+      hipLaunchKernelGGL((dattn::merge_oproj_kernel<128, 4>), grid, block, mlds, stream, p);
+    }
+    return (int)hipGetLastError();
+  }
+  const size_t lds = (size_t)nwv * dattn::KB * D * 2 + (size_t)nwv * 16 * D * 4 + (size_t)2 * nwv * 16 * 4;
   static const bool wo_late = [] {
     const char* e = getenv("NXD_DECODE_WO_LATE");
     return e ? atoi(e) != 0 : true;

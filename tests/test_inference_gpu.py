@@ -1,6 +1,8 @@
 """Inference on MI355X: fused-kernel prefill vs fp32 CPU reference, hipGraph decode loop == eager
 decode, sampling under graphs."""
 
+import os
+
 import pytest
 import torch
 
@@ -261,9 +263,10 @@ def test_fused_attention_oproj_matches_two_launches(monkeypatch, hidden, heads, 
 
 @pytest.mark.parametrize("hidden,heads,kv", [(2048, 32, 8), (1024, 8, 2)])   # D = 64, 128
 def test_fused_attention_oproj_long_context(monkeypatch, hidden, heads, kv):
-    """The fused attention + o_proj launch on a cache past one 1,024-key split (the notebook config's
-    2,048-token context + 256 new): each workgroup walks the whole cache; one decode step against the
-    split attention + merge + o_proj launches on identical caches."""
+    """The fused attention + o_proj launches on a cache past one 1,024-key split (the notebook config's
+    2,048-token context + 256 new) -- every workgroup walking the whole cache, and the default split
+    attention whose partials the o_proj launch merges -- one decode step each against the split
+    attention + merge + o_proj launches on identical caches."""
     from transformers import LlamaConfig, LlamaForCausalLM as HF
     from neuronx_distributed_llama3_2_amd.inference import model_base
 
@@ -283,14 +286,26 @@ def test_fused_attention_oproj_long_context(monkeypatch, hidden, heads, kv):
     sid = torch.arange(2, device="cuda")
     clen = torch.full((2,), P + 2, dtype=torch.int32, device="cuda")
     saved = f.kv_cache.clone()
-    monkeypatch.setattr(model_base, "_ATTN_OPROJ", True)
-    lf = f.forward_tokens(last, pos, sid, clen).float()
-    buf = getattr(f, "_oacc_buf", None)
-    assert buf is not None and int((buf != 0).sum()) == 0, "fused path not taken or accumulator not consumed"
-    f.kv_cache.copy_(saved)
-    monkeypatch.setattr(model_base, "_ATTN_OPROJ", False)
-    lu = f.forward_tokens(last, pos, sid, clen).float()
-    assert ((lf - lu).abs().max() / lu.abs().max()).item() < 2e-2
+    from neuronx_distributed_llama3_2_amd.ops import ext as _native
+
+    def step(fuse, maxl):
+        f.kv_cache.copy_(saved)
+        monkeypatch.setattr(model_base, "_ATTN_OPROJ", fuse)
+        _native().decode_attn_set_oproj_maxl(maxl)
+        try:
+            out = f.forward_tokens(last, pos, sid, clen).float()
+        finally:
+            _native().decode_attn_set_oproj_maxl(int(os.environ.get("NXD_DECODE_ATTN_OPROJ_MAXL", "1024")))
+        if fuse:
+            buf = getattr(f, "_oacc_buf", None)
+            assert buf is not None and int((buf != 0).sum()) == 0, "fused path not taken or accumulator not consumed"
+        return out
+
+    lu = step(False, 1024)
+    lf = step(True, 4096)    # one pass over the whole cache per workgroup
+    ls = step(True, 1024)    # split attention partials, merged inside the o_proj launch
+    for got in (lf, ls):
+        assert ((got - lu).abs().max() / lu.abs().max()).item() < 2e-2
 
 
 @pytest.mark.parametrize("hidden,heads,batch,split", [(512, 8, 2, 0), (1024, 8, 4, 0), (2048, 32, 8, 0), (2048, 32, 8, 1)])
