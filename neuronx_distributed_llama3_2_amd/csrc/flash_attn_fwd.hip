@@ -23,6 +23,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace nxd {
 namespace fa {
@@ -73,6 +74,13 @@ __device__ __forceinline__ uint32_t lds_addr(const char* ptr) { return (uint32_t
 __device__ __forceinline__ short4_t tr_read(uint32_t a) {
   short4_t v;
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ short4_t tr_read_off(uint32_t a) {   // + an immediate byte offset
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+  short4_t v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
   return v;
 }
 template <int N>
@@ -189,9 +197,26 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
   // supplies row q, columns 4pp..4pp+3 of that block.
   const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
   const int g = lane >> 4;
+  // V transposed-read addresses without the tile part: row 32 j + 16 s2 + 4 hh + tq (+ 8) of
+  // buffer buf is this per-lane base + the immediate buf * 2 * TILE + TILE + (32 j + 16 s2) * 2D
+  // (the swizzle only sees row bits 0-3, which j and s2 do not touch)
+  uint32_t vlane[NDB][2];
+  {
+    const uint32_t s0 = lds_addr(smem);
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) {
+      const int col = 32 * db + 16 * (g & 1) + 4 * tp;
+      const int ch = col >> 3, sub = (col & 7) * 2;
+      vlane[db][0] = s0 + lds_off<D>(4 * hh + tq, ch) + sub;
+      vlane[db][1] = s0 + lds_off<D>(4 * hh + 8 + tq, ch) + sub;
+    }
+  }
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
+  // The tile loop is unrolled by the two LDS buffers: with the buffer a compile-time constant every
+  // K / V read address is a loop-invariant per-lane offset plus an immediate (buffer, 32-key subtile,
+  // 16-row P.V group), instead of a v_add_u32 per read on the tile's base.
+  auto tile = [&](int t, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
     // buffer buf^1 was last read in iteration t-1, which every wave finished before the
     // barrier that closed it: safe to refill now, overlapped with this tile's MFMAs.
     if (t + 1 < ntiles) issue_tile(t + 1, buf ^ 1);
@@ -201,7 +226,6 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
       const bool wave_active = kt0 <= wave_qmax || !p.causal;
       if (wave_active) {
         const char* kl = smem + buf * 2 * TILE_BYTES;
-        const char* vl = kl + TILE_BYTES;
         // ---- S^T for the two 32-key subtiles
         f32x16_t sacc[2];
         sacc[0] = f32x16_t{0};
@@ -223,23 +247,20 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
         }
         // V reads of the first two P.V groups go out now, hidden behind the softmax VALU work
         short4_t va[8], vb2[8];
-        const uint32_t vb = lds_addr(vl);
           // 4 groups (j, s2) of 8 transposed V reads (4 d-blocks x lo/hi); group g+1 is issued
           // before group g's MFMAs, a counted wait covers exactly group g
-          auto issue = [&](int grp, short4_t (&v)[8]) {
-            const int j = grp >> 1, s2 = grp & 1;
-            const int R0 = 32 * j + 16 * s2 + 4 * hh;
+          auto issue = [&](auto grpc, short4_t (&v)[8]) {
+            constexpr int grp = decltype(grpc)::value;
+            constexpr int OFF = buf * 2 * TILE_BYTES + TILE_BYTES + (32 * (grp >> 1) + 16 * (grp & 1)) * D * 2;
   #pragma unroll
             for (int db = 0; db < NDB; ++db) {
-              const int col = 32 * db + 16 * (g & 1) + 4 * tp;
-              const int ch = col >> 3, sub = (col & 7) * 2;
-              v[2 * db] = tr_read(vb + lds_off<D>(R0 + tq, ch) + sub);
-              v[2 * db + 1] = tr_read(vb + lds_off<D>(R0 + 8 + tq, ch) + sub);
+              v[2 * db] = tr_read_off<OFF>(vlane[db][0]);
+              v[2 * db + 1] = tr_read_off<OFF>(vlane[db][1]);
             }
           };
         static_assert(NDB <= 4, "group size is 8 reads");
-        issue(0, va);
-        issue(1, vb2);
+        issue(std::integral_constant<int, 0>{}, va);
+        issue(std::integral_constant<int, 1>{}, vb2);
         // ---- mask + tile max on the RAW scores (scale > 0 commutes with max); the scale is folded
         // into one FMA per score below: p = exp2(s * c - m*c)
         const bool need_mask = (kt0 + kBlockN > p.Sk) || (p.causal && kt0 + kBlockN - 1 > wave_qmin);
@@ -311,10 +332,10 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
           };
           tr_wait<2 * NDB>(va);
           mma(0, va);
-          issue(2, va);
+          issue(std::integral_constant<int, 2>{}, va);
           tr_wait<2 * NDB>(vb2);
           mma(1, vb2);
-          issue(3, vb2);
+          issue(std::integral_constant<int, 3>{}, vb2);
           tr_wait<2 * NDB>(va);
           mma(2, va);
           tr_wait<0>(vb2);
@@ -323,6 +344,10 @@ __global__ void __launch_bounds__(W * 64, 8 / W) fwd_kernel(FwdParams p) {
       }
     }
     __syncthreads();  // vmcnt(0) + barrier: tile t+1 has landed for every wave
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(t, std::integral_constant<int, 0>{});
+    if (t + 1 < ntiles) tile(t + 1, std::integral_constant<int, 1>{});
   }
 
   // ---- epilogue: O[q][d] = acc / l ; lse
