@@ -7,8 +7,8 @@ world of 1, hipGraph decode through the fused kernels).
 bf16 TP=2 and TP=1 round their partial sums differently (the row-parallel all-reduce adds two bf16
 partials), so a random-init model can flip a greedy argmax where its top-2 logits nearly tie.  The
 check: greedy tokens identical for all 64 new tokens -- or, at the first differing position,
-teacher-forced prefill logits of both servers agree (relative L2 and max errors <= 3.5e-2, just
-above the measured 2.8e-2) and, in each row that flips, TP=1's margin between its token and TP=2's token is within
+teacher-forced prefill logits of both servers agree (relative L2 and max errors <= 3.5e-2, ~10 %
+above the largest of 18 measured samples, profiles/r6_tp2_prefill_parity_distribution.jsonl) and, in each row that flips, TP=1's margin between its token and TP=2's token is within
 the two servers' logit differences at those two tokens (a genuine near-tie).  The
 "peaked" model (untied lm_head = a row permutation of the embedding: next token = pi(current) by a
 wide margin) must match exactly."""
@@ -100,8 +100,9 @@ def test_tp2_server_greedy_matches_tp1_on_gpu(kind):
             la, lb = la[:, -1], lb[:, -1]
         rel_l2 = (la - lb).norm() / la.norm()
         rel_max = (la - lb).abs().max() / la.abs().max()
-        # measured worst cases: rel_max 2.79e-2 (profiles/r4b_gpu_tests_spmd_flake.log), rel_l2 2.76e-2
-        # (round 5, gpurun_out/r5b): a small margin above them.  These are PREFILL logits (TP=2 adds its
+        # distribution over 3 weight seeds x 6 prompts (profiles/r6_tp2_prefill_parity_distribution.jsonl):
+        # Llama-3.2-1B rel_l2 p50 2.70e-2 / max 2.89e-2, rel_max p50 2.74e-2 / max 3.19e-2 (tiny model
+        # <= 5.9e-3); the bound sits ~10 % above the largest.  These are PREFILL logits (TP=2 adds its
         # row-parallel partials in bf16), the bound on the prefix that decides the divergence
         print(f"{kind}: first differing token at {diff} ({diff - 16} new tokens identical); prefill logits "
               f"rel_l2 {float(rel_l2):.4f} rel_max {float(rel_max):.4f}")
