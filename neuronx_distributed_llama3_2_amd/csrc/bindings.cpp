@@ -81,6 +81,8 @@ int dense_gemm_choose_splits(int, int, int);
 void dense_gemm_set_pipe(int);
 void decode_attn_set_oproj_maxl(int);
 int decode_attn_oproj_maxl();
+int decode_attn_sync_error(bool);
+void decode_attn_set_sync(int);
 void grouped_rowgemm_set_pp(int);
 void wgrad_gemm_set_pp(int);
 int cu_stream_launch(const void*, void*, int64_t, int, int64_t, hipStream_t);
@@ -1152,6 +1154,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("decode_attn", &decode_attn);
   m.def("decode_attn_oproj", &decode_attn_oproj);
+  m.def("decode_attn_sync_error", [](bool reset) { return nxd::decode_attn_sync_error(reset); }, py::arg("reset") = false);
+  m.def("decode_attn_set_sync", [](int64_t v) { nxd::decode_attn_set_sync((int)v); });
   m.def("decode_attn_set_oproj_maxl", [](int64_t v) { nxd::decode_attn_set_oproj_maxl((int)v); });
   m.def("decode_attn_prefetch", &decode_attn_prefetch);
   m.def("kv_cache_write", &kv_cache_write);

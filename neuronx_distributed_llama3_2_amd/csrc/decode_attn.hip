@@ -66,10 +66,18 @@ struct Params {
   // initialisation, so the field was stack garbage (non-null) there and the kernel stored through it
   // (profiles/r4_decode_attn_trace_abort.txt).  Every launcher now value-initialises its Params.
   uint64_t* trace;
+  // SYNC (fused, long caches): per-(batch, kv head) arrival / done counters [2][kSyncHeads] (device
+  // globals, zero at load, reset by the last workgroup of each head) and the bounded-spin error word
+  unsigned* sync_cnt;
+  int* sync_err;
 };
 static_assert(std::is_trivially_copyable<Params>::value && sizeof(Params) <= 4096, "kernel-argument struct");
 
 static uint64_t* g_trace = nullptr;
+
+constexpr int kSyncHeads = 4096;   // batch x kv heads covered by the SYNC counters
+__device__ unsigned g_sync_cnt[2 * kSyncHeads];
+__device__ int g_sync_err;
 
 // Prefetch workgroup body: 4 independent 16-B loads in flight per lane, folded into one value that
 // is stored only under a condition the host never creates (pf_n16[0] < 0), so the loads stay live.
@@ -133,8 +141,20 @@ __device__ __forceinline__ void oproj_tail(const Params& p, const float* of, con
   }
 }
 
-template <int D, int NWV, bool FUSE, bool WO_LATE = true>
+// SYNC (with FUSE, caches past one pass): workgroup r of a kv head's R also computes key split r
+// (kps keys; splits >= nsplit have none), publishes its (m, l, o) partial with write-through (sc1)
+// stores and an agent-scope arrival count, waits until the head's nsplit partials have arrived
+// (bounded spin: every workgroup of the grid is resident, the host caps the grid at the CU count),
+// merges them with sc1 loads and runs its o_proj slice: split-K attention + merge + o_proj in one
+// launch, the KV cache read once (the one-pass FUSE form re-reads it in all R workgroups, the
+// two-launch form pays a second kernel boundary).  The last workgroup of a head through the merge
+// resets the head's counters for the next launch.  Measured SLOWER than the two launches it replaces
+// at the notebook config (17.9 us vs 5.7 + 5.6 us per layer, 0.790 vs 0.682 ms/token: the in-launch
+// fan-in of 32 workgroups per head and the 4-byte write-through partial reads cost more than a kernel
+// boundary; profiles/r6_decode/sync_ab.txt), so it is off by default (NXD_DECODE_ATTN_SYNC=1).
+template <int D, int NWV, bool FUSE, bool WO_LATE = true, bool SYNC = false>
 __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
+  static_assert(!SYNC || FUSE, "SYNC is a FUSE form");
   constexpr int NS = D / 32;      // k-steps of the score MFMA
   constexpr int NDT = D / 16;     // 16-wide d tiles of the output
   constexpr int VL = D / 8;       // 16-B V loads per lane for 64 keys x D
@@ -151,7 +171,7 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
     return;
   }
   if (p.trace != nullptr && tid == 0) p.trace[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-  const int split = FUSE ? 0 : (int)blockIdx.x % p.nsplit;
+  const int split = FUSE ? (SYNC ? (int)blockIdx.x % p.R : 0) : (int)blockIdx.x % p.nsplit;
   const int bh = FUSE ? (int)blockIdx.x / p.R : (int)blockIdx.x / p.nsplit;
   const int b = bh / p.Hkv, hkv = bh % p.Hkv;
   const int G = p.Hq / p.Hkv, M = G * p.T;
@@ -189,7 +209,7 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
   for (int i = 0; i < NDT; ++i) o[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // FUSE: the whole cache in one pass per workgroup (no key splits, no merge launch)
-  const int kend = FUSE ? slen : min(slen, (split + 1) * p.kps);
+  const int kend = (FUSE && !SYNC) ? slen : min(slen, (split + 1) * p.kps);
   // K fragments and the V chunk of the NEXT chunk are loaded while this one runs its softmax and P.V
   u32x4_t kf[4][NS], vv[VL];
   auto load_chunk = [&](int k0) {
@@ -324,8 +344,17 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
       L += wt * red_l[w * 16 + m];
       acc += wt * red_o[(w * 16 + m) * D + d];
     }
-    if (FUSE) {   // bf16-rounded as the unfused path's attention output, then o_proj below
+    if (FUSE && !SYNC) {   // bf16-rounded as the unfused path's attention output, then o_proj below
       reinterpret_cast<float*>(smem)[m * D + d] = bf2f(f2bf(L > 0.f ? acc / L : 0.f));
+    } else if (SYNC) {   // write-through partials (the merge reads them from other workgroups)
+      if (split < p.nsplit) {
+        __hip_atomic_store(p.po + (pbase + m) * D + d, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == 0) {
+          __hip_atomic_store(p.pm + pbase + m, gm == -INFINITY ? -INFINITY : gm * 0.69314718056f, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(p.pl + pbase + m, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
     } else if (p.nsplit == 1) {
       const int tt = m / G, gg = m % G;
       p.out[(int64_t)b * p.o_sb + (int64_t)tt * p.o_st + (int64_t)(hkv * G + gg) * p.o_sh + d] =
@@ -335,6 +364,76 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
       if (d == 0) {
         p.pm[pbase + m] = gm == -INFINITY ? -INFINITY : gm * 0.69314718056f;   // log2 -> natural-log domain
         p.pl[pbase + m] = L;
+      }
+    }
+  }
+  if constexpr (SYNC) {
+    int& lost_s = *reinterpret_cast<int*>(red_m);   // red_m is free once the waves are merged (no static
+                                                     // __shared__: it would shift the dynamic LDS base)
+    // publish: every storing wave drains its write-through stores, then one arrival per workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      if (split < p.nsplit) __hip_atomic_fetch_add(p.sync_cnt + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int lost = 0;
+      for (unsigned spins = 0; __hip_atomic_load(p.sync_cnt + bh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                               (unsigned)p.nsplit;) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 24)) {   // ~0.5 s: a partial never arrived
+          lost = 1;
+          __hip_atomic_store(p.sync_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      lost_s = lost;
+    }
+    __syncthreads();
+    // merge the head's partials (every load write-through / sc1: no stale line from an earlier launch)
+    float* of = reinterpret_cast<float*>(smem);   // [M][D]
+    float* wts = of + 16 * D;                     // [nsplit][16]
+    const int ns = p.nsplit;
+    const int64_t pb = (int64_t)bh * ns * M;
+    for (int m = wid; m < M; m += NWV) {
+      float gm = -INFINITY;
+      for (int sp = lane; sp < ns; sp += 64)
+        gm = fmaxf(gm, __hip_atomic_load(p.pm + pb + (int64_t)sp * M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) gm = fmaxf(gm, __shfl_xor(gm, off, 64));
+      float L = 0.f;
+      for (int sp = lane; sp < ns; sp += 64) {
+        const float ms = __hip_atomic_load(p.pm + pb + (int64_t)sp * M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float w = ms == -INFINITY ? 0.f : __expf(ms - gm);
+        wts[sp * 16 + m] = w;
+        L += w * __hip_atomic_load(p.pl + pb + (int64_t)sp * M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) L += __shfl_xor(L, off, 64);
+      const float inv = L > 0.f ? 1.f / L : 0.f;
+      for (int sp = lane; sp < ns; sp += 64) wts[sp * 16 + m] *= inv;
+    }
+    __syncthreads();
+    for (int it = tid; it < M * D; it += 64 * NWV) {
+      const int m = it / D;
+      const float* src = p.po + (pb + m) * D + it % D;
+      const int64_t st = (int64_t)M * D;
+      float acc = 0.f;
+      int sp = 0;
+      for (; sp + 3 < ns; sp += 4) {
+        const float a0 = __hip_atomic_load(src + sp * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float a1 = __hip_atomic_load(src + (sp + 1) * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float a2 = __hip_atomic_load(src + (sp + 2) * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float a3 = __hip_atomic_load(src + (sp + 3) * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc += wts[sp * 16 + m] * a0 + wts[(sp + 1) * 16 + m] * a1 + wts[(sp + 2) * 16 + m] * a2 + wts[(sp + 3) * 16 + m] * a3;
+      }
+      for (; sp < ns; ++sp) acc += wts[sp * 16 + m] * __hip_atomic_load(src + sp * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      of[it] = lost_s ? __builtin_nanf("") : bf2f(f2bf(acc));
+    }
+    __syncthreads();   // every partial this workgroup reads has been consumed
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(p.sync_cnt + kSyncHeads + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == (unsigned)p.R - 1) {   // the head's last workgroup: every peer is past its wait and its reads
+        __hip_atomic_store(p.sync_cnt + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p.sync_cnt + kSyncHeads + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -375,29 +474,99 @@ __global__ void __launch_bounds__(64 * NWV) merge_oproj_kernel(Params p) {
   const int G = p.Hq / p.Hkv, M = G * p.T;
   const int tpr = (G * D) / 32, seg = tid % tpr, r0 = tid / tpr, rpp = (64 * NWV) / tpr;
   const int row0 = ((int)blockIdx.x % p.R) * (p.Hout / p.R) + r0;
+  const int64_t pb = (int64_t)bh * p.nsplit * M;
+  const int ns = p.nsplit, lane = tid & 63, wid = tid >> 6;
+  // the splits are divided over H thread groups (partials summed through LDS); when a thread's share
+  // fits in registers its partial-row loads are issued first, beside the stats loads below, so the
+  // merge costs one memory round trip instead of two
+  constexpr int PMAX = 16;
+  const int elems = M * D, H = (64 * NWV) / elems >= 2 ? 2 : 1;
+  const int64_t st = (int64_t)M * D;   // one split further
+  const bool regs = elems * H <= 64 * NWV && (ns + H - 1) / H <= PMAX;
+  const int e0 = tid % elems, h0 = tid / elems;
+  const float* src0 = p.po + (pb + e0 / D) * D + e0 % D;
+  float pv[PMAX];
+  if (regs && tid < elems * H) {
+#pragma unroll
+    for (int i = 0; i < PMAX; ++i)
+      if (h0 + i * H < ns) pv[i] = src0[(h0 + i * H) * st];
+  }
+  // split weights of query row m: one wave per row, one split per lane (all loads in parallel: a
+  // serial walk over the splits was a chain of dependent L2 round trips, 7.8 us per launch).  The
+  // stats are loaded before the Wo block, whose HBM latency then hides behind the merge (vmcnt
+  // retires in issue order: issued first, Wo would gate the first use of the stats)
+  constexpr int KM = (16 + NWV - 1) / NWV;   // rows per wave (M <= 16)
+  const bool fast = regs && ns <= 64;
+  float pmv[KM], plv[KM];
+  if (fast) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int m = wid + k * NWV;
+      const bool ok = m < M && lane < ns;
+      pmv[k] = ok ? p.pm[pb + (int64_t)lane * M + m] : -INFINITY;
+      plv[k] = ok ? p.pl[pb + (int64_t)lane * M + m] : 0.f;
+    }
+  }
   u32x4_t wreg[4][4];
   load_wo_regs(p, row0, hkv * G * D + 32 * seg, rpp, wreg);
-  const int64_t pb = (int64_t)bh * p.nsplit * M;
-  if (tid < M) {
-    float gm = -INFINITY;
-    for (int s = 0; s < p.nsplit; ++s) gm = fmaxf(gm, p.pm[pb + (int64_t)s * M + tid]);
-    float L = 0.f;
-    for (int s = 0; s < p.nsplit; ++s) {
-      const float ms = p.pm[pb + (int64_t)s * M + tid];
-      const float w = ms == -INFINITY ? 0.f : __expf(ms - gm);
-      wts[s * 16 + tid] = w;
-      L += w * p.pl[pb + (int64_t)s * M + tid];
+  if (fast) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int m = wid + k * NWV;
+      if (m >= M) break;   // wave-uniform
+      float gm = pmv[k];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) gm = fmaxf(gm, __shfl_xor(gm, off, 64));
+      const float w = pmv[k] == -INFINITY ? 0.f : __expf(pmv[k] - gm);
+      float L = w * plv[k];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) L += __shfl_xor(L, off, 64);
+      if (lane < ns) wts[lane * 16 + m] = L > 0.f ? w / L : 0.f;
     }
+  } else for (int m = wid; m < M; m += NWV) {
+    float gm = -INFINITY;
+    for (int s = lane; s < ns; s += 64) gm = fmaxf(gm, p.pm[pb + (int64_t)s * M + m]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) gm = fmaxf(gm, __shfl_xor(gm, off, 64));
+    float L = 0.f;
+    for (int s = lane; s < ns; s += 64) {
+      const float ms = p.pm[pb + (int64_t)s * M + m];
+      const float w = ms == -INFINITY ? 0.f : __expf(ms - gm);
+      wts[s * 16 + m] = w;
+      L += w * p.pl[pb + (int64_t)s * M + m];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) L += __shfl_xor(L, off, 64);
     const float inv = L > 0.f ? 1.f / L : 0.f;
-    for (int s = 0; s < p.nsplit; ++s) wts[s * 16 + tid] *= inv;
+    for (int s = lane; s < ns; s += 64) wts[s * 16 + m] *= inv;
   }
   __syncthreads();
-  for (int it = tid; it < M * D; it += 64 * NWV) {
-    const int m = it / D, d = it % D;
+  // weighted sum of the partial rows
+  float* part = wts + ns * 16;   // [H][M * D]
+  if (regs) {
+    if (tid < elems * H) {
+      const int m = e0 / D;
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < PMAX; ++i)
+        if (h0 + i * H < ns) acc += wts[(h0 + i * H) * 16 + m] * pv[i];
+      part[h0 * elems + e0] = acc;
+    }
+  } else for (int it = tid; it < elems * H; it += 64 * NWV) {   // four independent loads in flight per thread
+    const int e = it % elems, h = it / elems, m = e / D, d = e % D;
+    const float* src = p.po + (pb + m) * D + d;
     float acc = 0.f;
-    for (int s = 0; s < p.nsplit; ++s) acc += wts[s * 16 + m] * p.po[(pb + (int64_t)s * M + m) * D + d];
-    of[it] = bf2f(f2bf(acc));
+    int sp = h;
+    for (; sp + 3 * H < ns; sp += 4 * H) {
+      const float a0 = src[sp * st], a1 = src[(sp + H) * st], a2 = src[(sp + 2 * H) * st], a3 = src[(sp + 3 * H) * st];
+      acc += wts[sp * 16 + m] * a0 + wts[(sp + H) * 16 + m] * a1 + wts[(sp + 2 * H) * 16 + m] * a2 +
+             wts[(sp + 3 * H) * 16 + m] * a3;
+    }
+    for (; sp < ns; sp += H) acc += wts[sp * 16 + m] * src[sp * st];
+    part[h * elems + e] = acc;
   }
+  __syncthreads();
+  for (int e = tid; e < elems; e += 64 * NWV) of[e] = bf2f(f2bf(H == 2 ? part[e] + part[elems + e] : part[e]));
   __syncthreads();
   oproj_tail<D>(p, of, wreg, b, row0, rpp, tpr, seg, G);
 }
@@ -470,8 +639,22 @@ int decode_attn2_launch(const void* q, const int64_t* qs, const void* kc, const 
 
 namespace dattn {
 int g_oproj_maxl = -1;   // NXD_DECODE_ATTN_OPROJ_MAXL, or decode_attn_set_oproj_maxl
+int g_sync_on = -1;      // NXD_DECODE_ATTN_SYNC (default 0: measured slower), or decode_attn_set_sync
 }
+void decode_attn_set_sync(int v) { dattn::g_sync_on = v ? 1 : 0; }
 void decode_attn_set_oproj_maxl(int v) { dattn::g_oproj_maxl = v; }
+
+// Bounded-spin error word of the SYNC launches (a partial never arrived: that launch wrote NaN);
+// reset clears it.  Synchronous (reads device memory).
+int decode_attn_sync_error(bool reset) {
+  int v = 0;
+  (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(dattn::g_sync_err), sizeof(int), 0, hipMemcpyDeviceToHost);
+  if (reset && v) {
+    const int z = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(dattn::g_sync_err), &z, sizeof(int), 0, hipMemcpyHostToDevice);
+  }
+  return v;
+}
 int decode_attn_oproj_maxl() {
   if (dattn::g_oproj_maxl < 0) {
     const char* e = getenv("NXD_DECODE_ATTN_OPROJ_MAXL");
@@ -525,9 +708,42 @@ int decode_attn_oproj_launch(const void* q, const int64_t* qs, const void* kc, c
   p.attn_wgs = B * Hkv * R;
   p.trace = dattn::g_trace;
   const dim3 grid(p.attn_wgs), block(nt);
+  if (dattn::g_sync_on < 0) {
+    const char* e = getenv("NXD_DECODE_ATTN_SYNC");
+    dattn::g_sync_on = e ? (atoi(e) != 0) : 0;
+  }
+  const bool sync_on = dattn::g_sync_on != 0;
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n;
+  }();
+  if (split && sync_on && B * Hkv <= dattn::kSyncHeads && (int)grid.x <= n_cu) {
+    // one launch: workgroup r of a head computes key split r (>= 128 keys, the partial buffers hold
+    // Lmax / 128 splits), then merges the head's splits and runs its o_proj slice (SYNC above)
+    int kps = (Lmax + R - 1) / R;
+    kps = (kps + dattn::KB - 1) / dattn::KB * dattn::KB;
+    kps = kps < 128 ? 128 : kps;
+    const int ns = (Lmax + kps - 1) / kps;
+    const size_t lds = (size_t)nwv * dattn::KB * D * 2 + (size_t)nwv * 16 * D * 4 + (size_t)2 * nwv * 16 * 4;
+    if (ns <= R && (size_t)16 * D * 4 + (size_t)ns * 16 * 4 <= (size_t)nwv * dattn::KB * D * 2) {
+      static unsigned* cnt = [] { void* a = nullptr; (void)hipGetSymbolAddress(&a, HIP_SYMBOL(dattn::g_sync_cnt)); return (unsigned*)a; }();
+      static int* err = [] { void* a = nullptr; (void)hipGetSymbolAddress(&a, HIP_SYMBOL(dattn::g_sync_err)); return (int*)a; }();
+      p.kps = kps; p.nsplit = ns; p.po = po; p.pm = pm; p.pl = pl; p.sync_cnt = cnt; p.sync_err = err;
+      if (D == 64) {
+        (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<64, 8, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((dattn::attn_kernel<64, 8, true, true, true>), grid, block, lds, stream, p);
+      } else {
+        (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<128, 4, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((dattn::attn_kernel<128, 4, true, true, true>), grid, block, lds, stream, p);
+      }
+      return (int)hipGetLastError();
+    }
+  }
   if (split) {
     const int kps = dattn::keys_per_split(Lmax, B, Hkv), ns = (Lmax + kps - 1) / kps;
-    const size_t mlds = (size_t)16 * D * 4 + (size_t)ns * 16 * 4;
+    const size_t mlds = (size_t)16 * D * 4 + (size_t)ns * 16 * 4 + (size_t)2 * 16 * D * 4;
     if (mlds > 64 * 1024) return -1;
     int ns2 = 0;
     const int64_t no_out[3] = {0, 0, 0};

@@ -483,6 +483,8 @@ class LlamaForCausalLMInference:
                     if bool(seen.any(1).all()):
                         break
             new.append(st.out[:, :min(done_steps, todo)].clone())
+            if hasattr(self.model, "check_decode_kernels"):
+                self.model.check_decode_kernels()
         out = torch.cat(new, 1)[:, :max_new_tokens]
         if eos.numel():
             hit = torch.isin(out, eos).int()

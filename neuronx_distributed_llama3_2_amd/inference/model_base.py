@@ -273,6 +273,15 @@ class DecoderInferenceMixin:
             return False
         return isinstance(self._decode_tp_state(ew.shape[1], ew.device)["ar"], PeerAllReduce)
 
+    def check_decode_kernels(self) -> None:
+        """Raise if a single-launch long-context attention + o_proj (csrc/decode_attn.hip SYNC) timed out
+        waiting for a key split's partial (that launch wrote NaN): read once per generate()."""
+        if not torch.cuda.is_available() or not ops.ext_available():
+            return
+        if ops.ext().decode_attn_sync_error(True):
+            raise RuntimeError("decode attention: a key-split partial never arrived (bounded spin timed out); "
+                               "the step's outputs are NaN")
+
     def check_collectives(self) -> None:
         """Raise if the TP decode all-reduce lost a peer since it was built (a pinned host word: the
         caller synchronises first so its own step is covered)."""

@@ -264,8 +264,9 @@ def test_fused_attention_oproj_matches_two_launches(monkeypatch, hidden, heads, 
 @pytest.mark.parametrize("hidden,heads,kv", [(2048, 32, 8), (1024, 8, 2)])   # D = 64, 128
 def test_fused_attention_oproj_long_context(monkeypatch, hidden, heads, kv):
     """The fused attention + o_proj launches on a cache past one 1,024-key split (the notebook config's
-    2,048-token context + 256 new) -- every workgroup walking the whole cache, and the default split
-    attention whose partials the o_proj launch merges -- one decode step each against the split
+    2,048-token context + 256 new) -- every workgroup walking the whole cache; the default single launch
+    whose workgroups each take a key split, wait for the head's partials and merge them; and the split
+    attention launch whose partials the o_proj launch merges -- one decode step each against the split
     attention + merge + o_proj launches on identical caches."""
     from transformers import LlamaConfig, LlamaForCausalLM as HF
     from neuronx_distributed_llama3_2_amd.inference import model_base
@@ -288,14 +289,17 @@ def test_fused_attention_oproj_long_context(monkeypatch, hidden, heads, kv):
     saved = f.kv_cache.clone()
     from neuronx_distributed_llama3_2_amd.ops import ext as _native
 
-    def step(fuse, maxl):
+    def step(fuse, maxl, sync=1):
         f.kv_cache.copy_(saved)
         monkeypatch.setattr(model_base, "_ATTN_OPROJ", fuse)
         _native().decode_attn_set_oproj_maxl(maxl)
+        _native().decode_attn_set_sync(sync)
         try:
             out = f.forward_tokens(last, pos, sid, clen).float()
         finally:
             _native().decode_attn_set_oproj_maxl(int(os.environ.get("NXD_DECODE_ATTN_OPROJ_MAXL", "1024")))
+            _native().decode_attn_set_sync(int(os.environ.get("NXD_DECODE_ATTN_SYNC", "0")))
+        assert _native().decode_attn_sync_error(True) == 0
         if fuse:
             buf = getattr(f, "_oacc_buf", None)
             assert buf is not None and int((buf != 0).sum()) == 0, "fused path not taken or accumulator not consumed"
@@ -303,8 +307,9 @@ def test_fused_attention_oproj_long_context(monkeypatch, hidden, heads, kv):
 
     lu = step(False, 1024)
     lf = step(True, 4096)    # one pass over the whole cache per workgroup
-    ls = step(True, 1024)    # split attention partials, merged inside the o_proj launch
-    for got in (lf, ls):
+    ls = step(True, 1024, sync=1)   # one launch: key split per workgroup, in-launch merge, o_proj (opt-in)
+    l2 = step(True, 1024, sync=0)   # split attention launch, partials merged inside the o_proj launch
+    for got in (lf, ls, l2):
         assert ((got - lu).abs().max() / lu.abs().max()).item() < 2e-2
 
 
