@@ -71,7 +71,7 @@ int grouped_gemm_launch(int, const void*, const void*, void*, const int*, int, i
 int wgrad_gemm_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int, int, int, int, hipStream_t);
 int wgrad_gemm_choose_splits(int, int, int);
 int decode_attn_oproj_launch(const void*, const int64_t*, const void*, const void*, const int64_t*, const int*, const int*,
-                             const void*, int64_t, int, float*, float*, float*, float*, int, int, int, int, int, int, float, hipStream_t);
+                             const void*, int64_t, int, float*, float*, float*, float*, float*, int, int, int, int, int, int, float, hipStream_t);
 int grouped_rowgemm_launch(int, const void*, const void*, void*, const int*, int, int, int, int, hipStream_t);
 int wgrad_gemm_grouped_launch(const void*, int64_t, const void*, int64_t, float*, int64_t, int64_t, const int*, int, int,
                               int, int, hipStream_t);
@@ -520,14 +520,15 @@ bool decode_attn_oproj(at::Tensor q, at::Tensor kc, at::Tensor vc, c10::optional
   // past the fused kernel's one-pass limit: split attention partials (keys per split >= 128), merged
   // inside the o_proj launch
   at::Tensor part;
-  float *po = nullptr, *pm = nullptr, *pl = nullptr;
+  float *po = nullptr, *pm = nullptr, *pl = nullptr, *mo = nullptr;
   if (Lmax > nxd::decode_attn_oproj_maxl()) {
-    const int64_t rows = (int64_t)B * Hkv * ((Lmax + 127) / 128) * ((int64_t)(Hq / Hkv) * T);
-    part = at::empty({rows * (D + 2)}, q.options().dtype(at::kFloat));
-    po = part.data_ptr<float>(); pm = po + rows * D; pl = pm + rows;
+    const int64_t M = (int64_t)(Hq / Hkv) * T;
+    const int64_t rows = (int64_t)B * Hkv * ((Lmax + 127) / 128) * M;
+    part = at::empty({rows * (D + 2) + (int64_t)B * Hkv * M * D}, q.options().dtype(at::kFloat));
+    po = part.data_ptr<float>(); pm = po + rows * D; pl = pm + rows; mo = pl + rows;
   }
   const int rc = nxd::decode_attn_oproj_launch(q.data_ptr(), qs, kc.data_ptr(), vc.data_ptr(), cs, ci, seq_len.data_ptr<int>(),
-                                               wo.data_ptr(), wo.stride(0), (int)Hout, oacc.data_ptr<float>(), po, pm, pl, B, T,
+                                               wo.data_ptr(), wo.stride(0), (int)Hout, oacc.data_ptr<float>(), po, pm, pl, mo, B, T,
                                                Hq, Hkv, D, Lmax, (float)scale, cur_stream());
   if (rc == -1) return false;
   check_rc(rc, "decode_attn_oproj");

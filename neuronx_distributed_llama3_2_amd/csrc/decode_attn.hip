@@ -70,13 +70,14 @@ struct Params {
   // globals, zero at load, reset by the last workgroup of each head) and the bounded-spin error word
   unsigned* sync_cnt;
   int* sync_err;
+  float* mo;          // SYNC: [B * Hkv, M, D] merged attention rows (the merger's hand-off)
 };
 static_assert(std::is_trivially_copyable<Params>::value && sizeof(Params) <= 4096, "kernel-argument struct");
 
 static uint64_t* g_trace = nullptr;
 
 constexpr int kSyncHeads = 4096;   // batch x kv heads covered by the SYNC counters
-__device__ unsigned g_sync_cnt[2 * kSyncHeads];
+__device__ unsigned g_sync_cnt[3 * kSyncHeads];   // arrivals, done, merged-flag per head
 __device__ int g_sync_err;
 
 // Prefetch workgroup body: 4 independent 16-B loads in flight per lane, folded into one value that
@@ -142,16 +143,16 @@ __device__ __forceinline__ void oproj_tail(const Params& p, const float* of, con
 }
 
 // SYNC (with FUSE, caches past one pass): workgroup r of a kv head's R also computes key split r
-// (kps keys; splits >= nsplit have none), publishes its (m, l, o) partial with write-through (sc1)
-// stores and an agent-scope arrival count, waits until the head's nsplit partials have arrived
-// (bounded spin: every workgroup of the grid is resident, the host caps the grid at the CU count),
-// merges them with sc1 loads and runs its o_proj slice: split-K attention + merge + o_proj in one
-// launch, the KV cache read once (the one-pass FUSE form re-reads it in all R workgroups, the
-// two-launch form pays a second kernel boundary).  The last workgroup of a head through the merge
-// resets the head's counters for the next launch.  Measured SLOWER than the two launches it replaces
-// at the notebook config (17.9 us vs 5.7 + 5.6 us per layer, 0.790 vs 0.682 ms/token: the in-launch
-// fan-in of 32 workgroups per head and the 4-byte write-through partial reads cost more than a kernel
-// boundary; profiles/r6_decode/sync_ab.txt), so it is off by default (NXD_DECODE_ATTN_SYNC=1).
+// (kps keys; splits >= nsplit have none) and publishes its (m, l, o) partial with write-through (sc1)
+// stores and an agent-scope arrival count; the split whose arrival completes the count merges the
+// head once and publishes the merged rows (write-through) and a flag, which the head's other
+// workgroups poll (bounded spin: every workgroup of the grid is resident, the host caps the grid at
+// the CU count) before their o_proj slices: split-K attention + merge + o_proj in one launch, the KV
+// cache read once.  The last workgroup of a head through the hand-off resets the head's counters.
+// Measured SLOWER than the two launches it replaces at the notebook config (16.1 us per layer --
+// 17.9 with every workgroup merging all partials itself -- vs 5.7 + 5.6 us; 0.759 vs 0.686
+// ms/token; profiles/r6_decode/sync_ab.txt): the in-launch wait on the slowest split of a head costs
+// more than a kernel boundary, so it is off by default (NXD_DECODE_ATTN_SYNC=1).
 template <int D, int NWV, bool FUSE, bool WO_LATE = true, bool SYNC = false>
 __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
   static_assert(!SYNC || FUSE, "SYNC is a FUSE form");
@@ -368,72 +369,93 @@ __global__ void __launch_bounds__(64 * NWV) attn_kernel(Params p) {
     }
   }
   if constexpr (SYNC) {
-    int& lost_s = *reinterpret_cast<int*>(red_m);   // red_m is free once the waves are merged (no static
-                                                     // __shared__: it would shift the dynamic LDS base)
-    // publish: every storing wave drains its write-through stores, then one arrival per workgroup
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      if (split < p.nsplit) __hip_atomic_fetch_add(p.sync_cnt + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int lost = 0;
-      for (unsigned spins = 0; __hip_atomic_load(p.sync_cnt + bh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                               (unsigned)p.nsplit;) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 24)) {   // ~0.5 s: a partial never arrived
-          lost = 1;
-          __hip_atomic_store(p.sync_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-      lost_s = lost;
-    }
-    __syncthreads();
-    // merge the head's partials (every load write-through / sc1: no stale line from an earlier launch)
-    float* of = reinterpret_cast<float*>(smem);   // [M][D]
+    int* flg = reinterpret_cast<int*>(red_m);   // [0] lost, [1] merger: red_m is free once the waves are
+                                                // merged (no static __shared__: it would shift the LDS base)
+    float* of = reinterpret_cast<float*>(smem);   // [M][D] merged attention output
     float* wts = of + 16 * D;                     // [nsplit][16]
     const int ns = p.nsplit;
     const int64_t pb = (int64_t)bh * ns * M;
-    for (int m = wid; m < M; m += NWV) {
-      float gm = -INFINITY;
-      for (int sp = lane; sp < ns; sp += 64)
-        gm = fmaxf(gm, __hip_atomic_load(p.pm + pb + (int64_t)sp * M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) gm = fmaxf(gm, __shfl_xor(gm, off, 64));
-      float L = 0.f;
-      for (int sp = lane; sp < ns; sp += 64) {
-        const float ms = __hip_atomic_load(p.pm + pb + (int64_t)sp * M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const float w = ms == -INFINITY ? 0.f : __expf(ms - gm);
-        wts[sp * 16 + m] = w;
-        L += w * __hip_atomic_load(p.pl + pb + (int64_t)sp * M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) L += __shfl_xor(L, off, 64);
-      const float inv = L > 0.f ? 1.f / L : 0.f;
-      for (int sp = lane; sp < ns; sp += 64) wts[sp * 16 + m] *= inv;
+    float* mo = p.mo + (int64_t)bh * M * D;       // the head's merged output, handed to its other workgroups
+    unsigned* cnt = p.sync_cnt + bh;
+    unsigned* done = p.sync_cnt + kSyncHeads + bh;
+    unsigned* flag = p.sync_cnt + 2 * kSyncHeads + bh;
+    // publish: every storing wave drains its write-through partial stores, then one arrival per split;
+    // the split whose arrival completes the count merges the head once
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      int merger = 0;
+      if (split < ns) merger = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)ns - 1;
+      flg[0] = 0;
+      flg[1] = merger;
     }
     __syncthreads();
-    for (int it = tid; it < M * D; it += 64 * NWV) {
-      const int m = it / D;
-      const float* src = p.po + (pb + m) * D + it % D;
-      const int64_t st = (int64_t)M * D;
-      float acc = 0.f;
-      int sp = 0;
-      for (; sp + 3 < ns; sp += 4) {
-        const float a0 = __hip_atomic_load(src + sp * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const float a1 = __hip_atomic_load(src + (sp + 1) * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const float a2 = __hip_atomic_load(src + (sp + 2) * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const float a3 = __hip_atomic_load(src + (sp + 3) * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        acc += wts[sp * 16 + m] * a0 + wts[(sp + 1) * 16 + m] * a1 + wts[(sp + 2) * 16 + m] * a2 + wts[(sp + 3) * 16 + m] * a3;
+    if (flg[1]) {
+      // every split's partial has arrived: merge (write-through / sc1 loads: no stale line from an
+      // earlier launch), publish the merged rows write-through, then the head's flag
+      for (int m = wid; m < M; m += NWV) {
+        float gm = -INFINITY;
+        for (int sp = lane; sp < ns; sp += 64)
+          gm = fmaxf(gm, __hip_atomic_load(p.pm + pb + (int64_t)sp * M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) gm = fmaxf(gm, __shfl_xor(gm, off, 64));
+        float L = 0.f;
+        for (int sp = lane; sp < ns; sp += 64) {
+          const float ms = __hip_atomic_load(p.pm + pb + (int64_t)sp * M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float w = ms == -INFINITY ? 0.f : __expf(ms - gm);
+          wts[sp * 16 + m] = w;
+          L += w * __hip_atomic_load(p.pl + pb + (int64_t)sp * M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) L += __shfl_xor(L, off, 64);
+        const float inv = L > 0.f ? 1.f / L : 0.f;
+        for (int sp = lane; sp < ns; sp += 64) wts[sp * 16 + m] *= inv;
       }
-      for (; sp < ns; ++sp) acc += wts[sp * 16 + m] * __hip_atomic_load(src + sp * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      of[it] = lost_s ? __builtin_nanf("") : bf2f(f2bf(acc));
+      __syncthreads();
+      for (int it = tid; it < M * D; it += 64 * NWV) {
+        const int m = it / D;
+        const float* src = p.po + (pb + m) * D + it % D;
+        const int64_t st = (int64_t)M * D;
+        float acc = 0.f;
+        int sp = 0;
+        for (; sp + 3 < ns; sp += 4) {
+          const float a0 = __hip_atomic_load(src + sp * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float a1 = __hip_atomic_load(src + (sp + 1) * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float a2 = __hip_atomic_load(src + (sp + 2) * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float a3 = __hip_atomic_load(src + (sp + 3) * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          acc += wts[sp * 16 + m] * a0 + wts[(sp + 1) * 16 + m] * a1 + wts[(sp + 2) * 16 + m] * a2 + wts[(sp + 3) * 16 + m] * a3;
+        }
+        for (; sp < ns; ++sp) acc += wts[sp * 16 + m] * __hip_atomic_load(src + sp * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float v = bf2f(f2bf(acc));
+        of[it] = v;
+        __hip_atomic_store(mo + it, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (tid == 0) {
+        for (unsigned spins = 0; __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1u << 24)) {   // ~0.5 s: the head's merge never arrived
+            flg[0] = 1;
+            __hip_atomic_store(p.sync_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      const bool lost = flg[0] != 0;
+      for (int it = tid; it < M * D; it += 64 * NWV)
+        of[it] = lost ? __builtin_nanf("") : __hip_atomic_load(mo + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __syncthreads();   // every partial this workgroup reads has been consumed
+    __syncthreads();   // the merged rows are in LDS: this workgroup is done with the hand-off
     if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add(p.sync_cnt + kSyncHeads + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (old == (unsigned)p.R - 1) {   // the head's last workgroup: every peer is past its wait and its reads
-        __hip_atomic_store(p.sync_cnt + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p.sync_cnt + kSyncHeads + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == (unsigned)p.R - 1) {   // the head's last workgroup: every peer has read the merged rows
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -672,8 +694,8 @@ int decode_attn_oproj_maxl() {
 // passes.
 int decode_attn_oproj_launch(const void* q, const int64_t* qs, const void* kc, const void* vc, const int64_t* cs,
                              const int* cache_idx, const int* seq_len, const void* wo, int64_t ldwo, int Hout, float* oacc,
-                             float* po, float* pm, float* pl, int B, int T, int Hq, int Hkv, int D, int Lmax, float scale,
-                             hipStream_t stream) {
+                             float* po, float* pm, float* pl, float* mo, int B, int T, int Hq, int Hkv, int D, int Lmax,
+                             float scale, hipStream_t stream) {
   if (Hkv <= 0 || Hq % Hkv) return -1;
   const int G = Hq / Hkv, M = G * T;
   const int maxl = decode_attn_oproj_maxl();
@@ -719,7 +741,7 @@ int decode_attn_oproj_launch(const void* q, const int64_t* qs, const void* kc, c
     (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     return n;
   }();
-  if (split && sync_on && B * Hkv <= dattn::kSyncHeads && (int)grid.x <= n_cu) {
+  if (split && sync_on && mo != nullptr && B * Hkv <= dattn::kSyncHeads && (int)grid.x <= n_cu) {
     // one launch: workgroup r of a head computes key split r (>= 128 keys, the partial buffers hold
     // Lmax / 128 splits), then merges the head's splits and runs its o_proj slice (SYNC above)
     int kps = (Lmax + R - 1) / R;
@@ -731,6 +753,7 @@ int decode_attn_oproj_launch(const void* q, const int64_t* qs, const void* kc, c
       static unsigned* cnt = [] { void* a = nullptr; (void)hipGetSymbolAddress(&a, HIP_SYMBOL(dattn::g_sync_cnt)); return (unsigned*)a; }();
       static int* err = [] { void* a = nullptr; (void)hipGetSymbolAddress(&a, HIP_SYMBOL(dattn::g_sync_err)); return (int*)a; }();
       p.kps = kps; p.nsplit = ns; p.po = po; p.pm = pm; p.pl = pl; p.sync_cnt = cnt; p.sync_err = err;
+      p.mo = mo;
       if (D == 64) {
         (void)hipFuncSetAttribute((const void*)dattn::attn_kernel<64, 8, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL((dattn::attn_kernel<64, 8, true, true, true>), grid, block, lds, stream, p);
