@@ -1,5 +1,6 @@
 // Decode attention on MFMA for small query groups (M = (Hq/Hkv) * T <= 16 rows per kv head):
-// one workgroup of 4 waves owns a (batch, kv head, key split of 1024 keys); every wave runs an
+// one workgroup (8 waves at D 64, 4 at D 128) owns a (batch, kv head, key split); the keys per split
+// (128-1,024, keys_per_split) are sized so the grid reaches ~128 workgroups; every wave runs an
 // online-softmax flash-decoding loop over 64-key chunks entirely in registers:
 //
 //   S^T[key][m] = K.Q^T   v_mfma_f32_16x16x32_bf16, K rows straight from the cache (16-B loads),
@@ -9,12 +10,14 @@
 //   O[m][d] += P.V      P re-packed into the A operand with 16 lane shuffles per chunk, V staged
 //                         through a per-wave LDS tile and read transposed (ds_read_b64_tr_b16);
 //
-// then the 4 waves merge their (max, sum, O) through LDS once.  With one split (cache <= 1024
-// keys) the workgroup writes the final bf16 output; otherwise it writes the (m, l, o) partials that
-// inference.hip's merge kernel combines.  Compared with the 128-key-chunk kernel there (four
-// workgroup barriers per chunk and a merge launch at every length) this is one barrier per call.
+// then the waves merge their (max, sum, O) through LDS once.  With one split the workgroup writes
+// the final bf16 output; otherwise it writes the (m, l, o) partials that inference.hip's merge kernel
+// -- or, fused with o_proj, merge_oproj_kernel below -- combines.  Compared with the 128-key-chunk
+// kernel there (four workgroup barriers per chunk and a merge launch at every length) this is one
+// barrier per call.
 //
-// FUSE (attention + o_proj, one launch instead of two): the grid is (batch, kv head, R row chunks
+// FUSE (attention + o_proj, one launch instead of two; caches up to NXD_DECODE_ATTN_OPROJ_MAXL =
+// 1,024 keys): the grid is (batch, kv head, R row chunks
 // of the o_proj output); every workgroup of a kv head recomputes that head group's attention (a
 // few hundred L2-resident keys at decode lengths) and multiplies it by its Wo block [H/R rows x
 // G*D columns], prefetched into registers before the attention starts, then adds the partial
@@ -31,7 +34,7 @@ namespace nxd {
 namespace dattn {
 
 constexpr int KB = 64;            // keys per chunk (one wave)
-constexpr int KPS = 1024;         // keys per workgroup split
+constexpr int KPS = 1024;         // most keys per workgroup split (one pass of 8 waves x 2 chunks)
 
 struct Params {
   const uint16_t* q;
